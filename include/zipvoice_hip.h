@@ -1,0 +1,123 @@
+/*
+ * zipvoice_hip.h — C ABI of the MI355X-native ZipVoice inference engine
+ * (libzipvoice_hip.so, gfx950).
+ *
+ * Plain pointers and sizes only.  Every tensor argument is a DEVICE pointer
+ * (caller-owned, row-major, contiguous) unless the parameter name says host_.
+ * All work is enqueued on `stream` (a hipStream_t, NULL = default stream); no
+ * call synchronises the host except zv_finalize (weight upload).
+ * Return value: 0 on success, nonzero on error; zv_last_error() then returns
+ * a thread-local message (the Python layer raises it as RuntimeError /
+ * ValueError, mirroring the reference's exceptions).
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference repository winlaic/ZipVoice):
+ *   zv_create / zv_set_weight / zv_finalize
+ *       ZipVoice*.__init__ + load_checkpoint(strict=True)
+ *       (zipvoice/models/zipvoice.py:38-133, zipvoice/utils/checkpoint.py:108-146,
+ *        zipvoice/bin/infer_zipvoice.py:549-566)
+ *   zv_fm_decoder      ZipVoice.forward_fm_decoder (zipvoice/models/zipvoice.py:135-185)
+ *                      == TTSZipformer.forward (zipvoice/models/modules/zipformer.py:242-293)
+ *   zv_velocity        DiffusionModel.forward / DistillDiffusionModel.forward
+ *                      (zipvoice/models/modules/solver.py:40-165)
+ *   zv_euler_sample    EulerSolver.sample (zipvoice/models/modules/solver.py:182-240)
+ *   zv_text_encode     ZipVoice.forward_text_embed (zipvoice/models/zipvoice.py:187-212,
+ *                      ZipVoiceDialog override zipvoice/models/zipvoice_dialog.py:127-159)
+ *   zv_text_condition  ZipVoice.forward_text_condition (zipvoice/models/zipvoice.py:214-251)
+ *   zv_speech_condition  speech-condition padding in ZipVoice.sample (zipvoice.py:441-451)
+ *   Reference per-step ONNX operator with the same contract as zv_velocity:
+ *       fm_decoder.onnx (zipvoice/bin/onnx_export.py:157-204)
+ */
+#ifndef ZIPVOICE_HIP_H
+#define ZIPVOICE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct zv_engine* zv_handle;
+
+enum zv_variant { ZV_ZIPVOICE = 0, ZV_DISTILL = 1, ZV_DIALOG = 2, ZV_DIALOG_STEREO = 3 };
+/* ZV_FP32: fp32-accurate mode (GEMMs as bf16x3 split products, fp32 everything else);
+ * ZV_BF16: bf16 MFMA operands, fp32 accumulation / residual stream / softmax. */
+enum zv_precision { ZV_FP32 = 0, ZV_BF16 = 1 };
+
+#define ZV_MAX_STACKS 8
+
+/* Mirrors the "model" block of model.json (egs/zipvoice/conf/zipvoice_base.json:2-25). */
+typedef struct {
+  int variant;                 /* zv_variant */
+  int precision;               /* zv_precision */
+  int feat_dim;                /* 100 */
+  int num_stacks;              /* len(fm_decoder_downsampling_factor) */
+  int downsampling_factor[ZV_MAX_STACKS];
+  int num_layers[ZV_MAX_STACKS];
+  int cnn_module_kernel[ZV_MAX_STACKS];
+  int fm_decoder_dim, fm_decoder_feedforward_dim, fm_decoder_num_heads;
+  int text_encoder_num_layers, text_encoder_feedforward_dim, text_encoder_cnn_module_kernel;
+  int text_encoder_num_heads, text_encoder_dim;
+  int time_embed_dim, text_embed_dim;
+  int query_head_dim, value_head_dim, pos_head_dim, pos_dim;
+  int vocab_size, pad_id, spk_a_id, spk_b_id;
+} zv_config;
+
+const char* zv_last_error(void);
+const char* zv_version(void);
+
+zv_handle zv_create(const zv_config* cfg);
+void zv_destroy(zv_handle h);
+
+/* Stage one state-dict tensor (host fp32, reference key name, e.g.
+ * "fm_decoder.encoders.1.encoder.layers.0.feed_forward2.in_proj.weight"). */
+int zv_set_weight(zv_handle h, const char* name, const float* host_data, int64_t numel);
+/* Check that every tensor of the config's state dict was staged (strict=True),
+ * convert/pad to the device layout and upload.  Synchronous. */
+int zv_finalize(zv_handle h);
+/* Pre-size the workspace for batches up to max_batch rows of max_frames frames
+ * (optional; forward calls grow it on demand, which synchronises). */
+int zv_reserve(zv_handle h, int max_batch, int max_frames);
+/* Total bytes of device memory held (weights + workspace). */
+int64_t zv_device_bytes(zv_handle h);
+
+/* Raw decoder: v = fm_decoder(cat[xt, text_c, speech_c], t, pad, g).
+ *  t:      [N] timesteps;  guidance: [N] (distill only, else NULL)
+ *  xt, speech_c: [N, T, Fx]; text_c: [N, T, feat_dim]; pad: [N, T] uint8 (1 = padded) or NULL
+ *  v_out:  [N, T, Fout] with Fout = Fx (stereo: stream chosen by input width). */
+int zv_fm_decoder(zv_handle h, const float* t, const float* guidance, const float* xt,
+                  const float* text_c, const float* speech_c, const uint8_t* pad, int N,
+                  int T, int Fx, float* v_out, void* stream);
+
+/* One guided velocity evaluation (solver.py:40-165): CFG doubling inside,
+ * x/text_c/speech_c/pad are the B un-doubled rows; v_out [B, T, Fx]. */
+int zv_velocity(zv_handle h, float t, float guidance_scale, const float* x,
+                const float* text_c, const float* speech_c, const uint8_t* pad, int B, int T,
+                float* v_out, void* stream);
+
+/* Full Euler ODE solve (solver.py:182-240), in place: x holds x0 on entry and
+ * x(t_end) on return.  Time grid: t_shift*u/(1+(t_shift-1)u), u = linspace. */
+int zv_euler_sample(zv_handle h, float* x, const float* text_c, const float* speech_c,
+                    const uint8_t* pad, int B, int T, int num_step, float guidance_scale,
+                    float t_start, float t_end, float t_shift, void* stream);
+
+/* Text encoder (+ dialog speaker-turn embeddings).
+ *  tokens: [B, S] int64 (already padded with pad_id, one extra pad per row);
+ *  pad: [B, S] uint8; spk: [B, S] int8 in {-1,0,1} (dialog only, else NULL);
+ *  out: [B, S, feat_dim]. */
+int zv_text_encode(zv_handle h, const int64_t* tokens, const uint8_t* pad,
+                   const int8_t* spk, int B, int S, float* out, void* stream);
+
+/* Frame-rate text condition: out[b, f] = embed[b, min(f / (T_b / S_b), S_b)].
+ *  tok_lens, feat_lens: [B] int32 device; out: [B, T, feat_dim]. */
+int zv_text_condition(zv_handle h, const float* embed, int B, int S, const int32_t* tok_lens,
+                      const int32_t* feat_lens, int T, float* out, void* stream);
+
+/* Speech condition: prompt features [B, Tp, F] padded/zeroed to [B, T, F]. */
+int zv_speech_condition(zv_handle h, const float* prompt, int B, int Tp, int F,
+                        const int32_t* prompt_lens, int T, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZIPVOICE_HIP_H */

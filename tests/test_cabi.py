@@ -1,0 +1,66 @@
+"""The C-ABI library builds, loads without a GPU and exports every symbol that
+include/zipvoice_hip.h declares (no compute calls here)."""
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "zipvoice_hip.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(zv_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_api():
+    syms = declared_symbols()
+    for s in ("zv_create", "zv_set_weight", "zv_finalize", "zv_fm_decoder", "zv_velocity",
+              "zv_euler_sample", "zv_text_encode", "zv_last_error", "zv_destroy"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    from zipvoice_amd.csrc.build import build
+    build(verbose=False)
+    from zipvoice_amd import engine
+    lib = engine.load_library()
+    syms = declared_symbols()
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(syms) == set(engine.SIGNATURES), "ctypes signature table out of sync"
+    assert lib.zv_version().decode().startswith("zipvoice_hip")
+
+
+def test_create_rejects_bad_config_without_gpu():
+    import ctypes
+    from zipvoice_amd import engine
+    from zipvoice_amd.config import default_config
+    lib = engine.load_library()
+    zc = engine.make_zv_config(default_config("zipvoice"), "fp32")
+    zc.num_stacks = 0
+    assert not lib.zv_create(ctypes.byref(zc))
+    assert "num_stacks" in lib.zv_last_error().decode()
+    # an engine handle can be created and staged on the host without a GPU
+    zc = engine.make_zv_config(default_config("zipvoice"), "bf16")
+    h = lib.zv_create(ctypes.byref(zc))
+    assert h
+    assert lib.zv_finalize(h) != 0           # strict: no weights staged
+    assert "missing weight" in lib.zv_last_error().decode()
+    lib.zv_destroy(h)
+
+
+def test_no_cpu_fallback():
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from zipvoice_amd.config import default_config
+    from zipvoice_amd.models import build_model
+    m = build_model(default_config("zipvoice"))
+    m.load_synthetic(0)
+    with pytest.raises(RuntimeError):
+        m.to("cuda:0")
+    with pytest.raises(RuntimeError):
+        m.to("cpu")

@@ -1,0 +1,83 @@
+// Shared device/host helpers for the ZipVoice MI355X (gfx950) engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <stdexcept>
+#include <string>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define ZV_CHECK(expr)                                                                  \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) +      \
+                               " at " __FILE__ ":" + std::to_string(__LINE__) + ": " #expr); \
+  } while (0)
+
+#define ZV_REQUIRE(cond, msg)                                                           \
+  do {                                                                                  \
+    if (!(cond)) throw std::invalid_argument(std::string(msg));                         \
+  } while (0)
+
+#define ZV_LAUNCH_CHECK() ZV_CHECK(hipGetLastError())
+
+// ---------------------------------------------------------------------------
+// numerics (scaling.py formulas, fp32)
+// ---------------------------------------------------------------------------
+
+// SwooshLForward, scaling.py:1174-1180: log(1+exp(x-4)) (x-4 if inf) - 0.08x - 0.035
+__device__ __forceinline__ float swoosh_l(float x) {
+  float xo = x - 4.0f;
+  float ls = logf(1.0f + expf(xo));
+  if (isinf(ls)) ls = xo;
+  return ls - 0.08f * x - 0.035f;
+}
+// SwooshRForward, scaling.py:1185-1191
+__device__ __forceinline__ float swoosh_r(float x) {
+  float xo = x - 1.0f;
+  float ls = logf(1.0f + expf(xo));
+  if (isinf(ls)) ls = xo;
+  return ls - 0.08f * x - 0.313261687f;
+}
+// SwooshR module (SwooshRFunction without k2), scaling.py:1106-1116:
+// logaddexp(0, x-1) - 0.08x - 0.313261687
+__device__ __forceinline__ float swoosh_r_lae(float x) {
+  float y = x - 1.0f;
+  float m = fmaxf(y, 0.0f);
+  return m + log1pf(expf(-fabsf(y))) - 0.08f * x - 0.313261687f;
+}
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+template <typename T> __device__ __forceinline__ float to_f(T v);
+template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ float to_f<bf16>(bf16 v) { return (float)v; }
+
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float v) { return (bf16)v; }
+
+// load 4 consecutive elements as floats (16-B for fp32, 8-B for bf16)
+__device__ __forceinline__ void load4(const float* p, float (&v)[4]) {
+  f32x4 t = *reinterpret_cast<const f32x4*>(p);
+  v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+}
+__device__ __forceinline__ void load4(const bf16* p, float (&v)[4]) {
+  bf16x4 t = *reinterpret_cast<const bf16x4*>(p);
+  v[0] = (float)t[0]; v[1] = (float)t[1]; v[2] = (float)t[2]; v[3] = (float)t[3];
+}
+__device__ __forceinline__ void store4(float* p, const float (&v)[4]) {
+  f32x4 t = {v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4*>(p) = t;
+}
+__device__ __forceinline__ void store4(bf16* p, const float (&v)[4]) {
+  bf16x4 t = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  *reinterpret_cast<bf16x4*>(p) = t;
+}
+
+__host__ __device__ static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+__host__ __device__ static inline long round_up(long a, long b) { return (a + b - 1) / b * b; }

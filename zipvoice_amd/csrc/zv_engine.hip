@@ -1,0 +1,798 @@
+// ZipVoice MI355X engine: weights, workspace, layer orchestration and the C ABI.
+//
+// Data layout in HBM: activations are (rows, channels) row-major with
+// rows = batch-major (b * L + l), i.e. (B, L, C); the reference's (L, B, C)
+// order inside the Zipformer is a layout choice, not a semantic one.  The
+// residual stream (src / cur) is always fp32; GEMM operands are bf16 (ZV_BF16)
+// or bf16 hi/lo pairs (ZV_FP32).  Weights are stored [Npad][Kpad] bf16 hi
+// (+ lo) zero-padded to the GEMM tile grid, biases fp32.
+#include <math.h>
+#include <string.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "zv_common.h"
+#include "zv_gemm.inc"
+#include "zv_attn.inc"
+#include "zv_elem.inc"
+#include "../../include/zipvoice_hip.h"
+
+static thread_local std::string g_last_error;
+
+namespace {
+
+constexpr int W_NPAD = 128;   // weight row padding (GEMM BN)
+constexpr int W_KPAD = 64;    // weight column padding (multiple of GEMM BK)
+
+struct Linear {
+  int N = 0, K = 0, Npad = 0, Kpad = 0;
+  bf16* hi = nullptr;
+  bf16* lo = nullptr;
+  float* w32 = nullptr;   // fp32 copy (small linears only)
+  float* b = nullptr;
+};
+
+struct LayerW {
+  Linear attn_in;
+  float* pos_w = nullptr;   // (H*pd, pos_dim)
+  Linear sa_in[2], sa_out[2];
+  Linear ff_in[3], ff_out[3];
+  Linear na_in, na_out;
+  Linear conv_in[2], conv_out[2];
+  float* dw_w[2] = {nullptr, nullptr};
+  float* dw_b[2] = {nullptr, nullptr};
+  int ks = 0;
+  float* bypass = nullptr;
+  float* bypass_mid = nullptr;
+  float* norm_bias = nullptr;
+  float norm_log_scale = 0.f;
+};
+
+struct StackW {
+  int ds = 1;
+  std::vector<LayerW> layers;
+  Linear time_emb;          // fp32 small linear (time_embed_dim -> dim)
+  float* ds_w = nullptr;    // softmax(downsample.bias)
+  float* combiner = nullptr;
+};
+
+struct ZipformerW {
+  int dim = 0, ff = 0, heads = 0, qd = 0, pd = 0, vd = 0, pos_dim = 0, temb_dim = -1;
+  std::vector<Linear> in_proj, out_proj;
+  std::vector<StackW> stacks;
+  bool has_time = false, has_guid = false;
+  Linear te0, te2, guid;    // fp32 small linears
+};
+
+// grow-only device buffer
+struct DBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  template <typename T> T* get(size_t n) {
+    size_t need = n * sizeof(T) + 256;
+    if (need > bytes) {
+      if (p) { ZV_CHECK(hipDeviceSynchronize()); ZV_CHECK(hipFree(p)); }
+      ZV_CHECK(hipMalloc(&p, need));
+      ZV_CHECK(hipMemset(p, 0, need));
+      bytes = need;
+    }
+    return reinterpret_cast<T*>(p);
+  }
+  ~DBuf() { if (p) (void)hipFree(p); }
+};
+
+struct Workspace {
+  DBuf xin, main, dsrc, cur, qkp, W, hidden, dwout, sa_v, sa_o, na_o;
+  DBuf temb0, temb1, tstack, tvec, gvec, posP, mask2, maskds, vout, emb;
+  size_t bytes() const {
+    size_t s = 0;
+    for (const DBuf* b : {&xin, &main, &dsrc, &cur, &qkp, &W, &hidden, &dwout, &sa_v, &sa_o, &na_o,
+                          &temb0, &temb1, &tstack, &tvec, &gvec, &posP, &mask2, &maskds, &vout,
+                          &emb})
+      s += b->bytes;
+    return s;
+  }
+};
+
+inline dim3 grid1d(long n, int block = 256) {
+  long g = (n + block - 1) / block;
+  if (g > 65536) g = 65536;
+  if (g < 1) g = 1;
+  return dim3((unsigned)g);
+}
+
+}  // namespace
+
+// ===========================================================================
+struct zv_engine {
+  zv_config cfg;
+  std::map<std::string, std::vector<float>> staged;
+  std::vector<void*> allocs;
+  size_t weight_bytes = 0;
+  bool ready = false;
+  ZipformerW dec, txt;
+  float* embed_table = nullptr;   // (vocab, text_embed_dim)
+  float* spk_table = nullptr;     // (2, feat_dim)
+  float* temb_freqs = nullptr;    // (time_embed_dim/2)
+  std::map<int, float*> pe_cache; // L -> (2L-1, pos_dim)
+  Workspace ws_dec, ws_txt;
+
+  explicit zv_engine(const zv_config& c) : cfg(c) {}
+  ~zv_engine() {
+    for (void* p : allocs) (void)hipFree(p);
+    for (auto& kv : pe_cache) (void)hipFree(kv.second);
+  }
+
+  // ---------------------------------------------------------------- weights
+  template <typename T> T* dalloc(size_t n) {
+    void* p = nullptr;
+    ZV_CHECK(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)));
+    allocs.push_back(p);
+    weight_bytes += n * sizeof(T);
+    return reinterpret_cast<T*>(p);
+  }
+  const std::vector<float>& take(const std::string& k, size_t numel) {
+    auto it = staged.find(k);
+    if (it == staged.end()) throw std::invalid_argument("missing weight: " + k);
+    if (it->second.size() != numel)
+      throw std::invalid_argument("weight " + k + ": expected " + std::to_string(numel) +
+                                  " elements, got " + std::to_string(it->second.size()));
+    return it->second;
+  }
+  float* upload_f32(const std::string& k, size_t numel) {
+    const auto& v = take(k, numel);
+    float* d = dalloc<float>(numel);
+    ZV_CHECK(hipMemcpy(d, v.data(), numel * sizeof(float), hipMemcpyHostToDevice));
+    return d;
+  }
+  Linear make_linear(const std::string& prefix, int N, int K, bool bias, bool keep_f32) {
+    Linear L;
+    L.N = N; L.K = K;
+    L.Npad = (int)round_up(N, W_NPAD);
+    L.Kpad = (int)round_up(K, W_KPAD);
+    const auto& w = take(prefix + ".weight", (size_t)N * K);
+    std::vector<bf16> hi((size_t)L.Npad * L.Kpad, (bf16)0.f), lo(hi.size(), (bf16)0.f);
+    for (int n = 0; n < N; ++n)
+      for (int k = 0; k < K; ++k) {
+        float v = w[(size_t)n * K + k];
+        bf16 h = (bf16)v;
+        hi[(size_t)n * L.Kpad + k] = h;
+        lo[(size_t)n * L.Kpad + k] = (bf16)(v - (float)h);
+      }
+    L.hi = dalloc<bf16>(hi.size());
+    L.lo = dalloc<bf16>(lo.size());
+    ZV_CHECK(hipMemcpy(L.hi, hi.data(), hi.size() * sizeof(bf16), hipMemcpyHostToDevice));
+    ZV_CHECK(hipMemcpy(L.lo, lo.data(), lo.size() * sizeof(bf16), hipMemcpyHostToDevice));
+    if (keep_f32) {
+      L.w32 = dalloc<float>((size_t)N * K);
+      ZV_CHECK(hipMemcpy(L.w32, w.data(), (size_t)N * K * sizeof(float), hipMemcpyHostToDevice));
+    }
+    if (bias) L.b = upload_f32(prefix + ".bias", N);
+    return L;
+  }
+  Linear make_small(const std::string& prefix, int N, int K, bool bias) {
+    Linear L;
+    L.N = N; L.K = K;
+    L.w32 = upload_f32(prefix + ".weight", (size_t)N * K);
+    if (bias) L.b = upload_f32(prefix + ".bias", N);
+    return L;
+  }
+
+  void build_zipformer(ZipformerW& Z, const std::string& pre, int dim, int ff, int heads,
+                       const std::vector<int>& ds, const std::vector<int>& layers,
+                       const std::vector<int>& ks, std::vector<int> in_dims,
+                       std::vector<int> out_dims, bool two_stream, int temb_dim, bool guid) {
+    Z.dim = dim; Z.ff = ff; Z.heads = heads;
+    Z.qd = cfg.query_head_dim; Z.pd = cfg.pos_head_dim; Z.vd = cfg.value_head_dim;
+    Z.pos_dim = cfg.pos_dim; Z.temb_dim = temb_dim;
+    ZV_REQUIRE(Z.qd == ATT_QD && Z.pd == ATT_PD, "engine supports query_head_dim=32, pos_head_dim=4");
+    for (size_t i = 0; i < in_dims.size(); ++i) {
+      std::string s = two_stream ? "." + std::to_string(i) : "";
+      Z.in_proj.push_back(make_linear(pre + "in_proj" + s, dim, in_dims[i], true, false));
+      Z.out_proj.push_back(make_linear(pre + "out_proj" + s, out_dims[i], dim, true, false));
+    }
+    const int qkp = (2 * Z.qd + Z.pd) * heads;
+    for (size_t s = 0; s < ds.size(); ++s) {
+      StackW S;
+      S.ds = ds[s];
+      std::string sp = pre + "encoders." + std::to_string(s) + ".";
+      std::string ep = S.ds != 1 ? sp + "encoder." : sp;
+      if (S.ds != 1) {
+        ZV_REQUIRE(S.ds <= 8, "downsampling factor > 8 unsupported");
+        const auto& b = take(sp + "downsample.bias", S.ds);
+        float mx = -INFINITY;
+        for (float v : b) mx = std::max(mx, v);
+        std::vector<float> w(S.ds);
+        float sum = 0.f;
+        for (int k = 0; k < S.ds; ++k) { w[k] = expf(b[k] - mx); sum += w[k]; }
+        for (int k = 0; k < S.ds; ++k) w[k] /= sum;
+        S.ds_w = dalloc<float>(S.ds);
+        ZV_CHECK(hipMemcpy(S.ds_w, w.data(), S.ds * sizeof(float), hipMemcpyHostToDevice));
+        S.combiner = upload_f32(sp + "out_combiner.bypass_scale", dim);
+      }
+      if (temb_dim > 0) S.time_emb = make_small(ep + "time_emb.1", dim, temb_dim, true);
+      for (int li = 0; li < layers[s]; ++li) {
+        std::string lp = ep + "layers." + std::to_string(li) + ".";
+        LayerW W;
+        W.attn_in = make_linear(lp + "self_attn_weights.in_proj", qkp, dim, true, false);
+        W.pos_w = upload_f32(lp + "self_attn_weights.linear_pos.weight",
+                             (size_t)heads * Z.pd * Z.pos_dim);
+        for (int a = 0; a < 2; ++a) {
+          std::string ap = lp + "self_attn" + std::to_string(a + 1) + ".";
+          W.sa_in[a] = make_linear(ap + "in_proj", heads * Z.vd, dim, true, false);
+          W.sa_out[a] = make_linear(ap + "out_proj", dim, heads * Z.vd, true, false);
+        }
+        const int hs[3] = {ff * 3 / 4, ff, ff * 5 / 4};
+        for (int f = 0; f < 3; ++f) {
+          std::string fp = lp + "feed_forward" + std::to_string(f + 1) + ".";
+          W.ff_in[f] = make_linear(fp + "in_proj", hs[f], dim, true, false);
+          W.ff_out[f] = make_linear(fp + "out_proj", dim, hs[f], true, false);
+        }
+        const int hid = 3 * dim / 4;
+        W.na_in = make_linear(lp + "nonlin_attention.in_proj", 3 * hid, dim, true, false);
+        W.na_out = make_linear(lp + "nonlin_attention.out_proj", dim, hid, true, false);
+        W.ks = ks[s];
+        for (int c = 0; c < 2; ++c) {
+          std::string cp = lp + "conv_module" + std::to_string(c + 1) + ".";
+          W.conv_in[c] = make_linear(cp + "in_proj", 2 * dim, dim, true, false);
+          W.conv_out[c] = make_linear(cp + "out_proj", dim, dim, true, false);
+          W.dw_w[c] = upload_f32(cp + "depthwise_conv.weight", (size_t)dim * W.ks);
+          W.dw_b[c] = upload_f32(cp + "depthwise_conv.bias", dim);
+        }
+        W.bypass = upload_f32(lp + "bypass.bypass_scale", dim);
+        W.bypass_mid = upload_f32(lp + "bypass_mid.bypass_scale", dim);
+        W.norm_bias = upload_f32(lp + "norm.bias", dim);
+        W.norm_log_scale = take(lp + "norm.log_scale", 1)[0];
+        S.layers.push_back(std::move(W));
+      }
+      Z.stacks.push_back(std::move(S));
+    }
+    if (temb_dim > 0) {
+      Z.has_time = true;
+      Z.te0 = make_small(pre + "time_embed.0", 2 * temb_dim, temb_dim, true);
+      Z.te2 = make_small(pre + "time_embed.2", temb_dim, 2 * temb_dim, true);
+      if (guid) {
+        Z.has_guid = true;
+        Z.guid = make_small(pre + "guidance_scale_embed", temb_dim, temb_dim, false);
+      }
+    }
+  }
+
+  bool stereo() const { return cfg.variant == ZV_DIALOG_STEREO; }
+  bool distill() const { return cfg.variant == ZV_DISTILL; }
+  bool dialog() const { return cfg.variant == ZV_DIALOG || cfg.variant == ZV_DIALOG_STEREO; }
+
+  void finalize() {
+    const int F = cfg.feat_dim;
+    std::vector<int> ds, nl, ks;
+    for (int s = 0; s < cfg.num_stacks; ++s) {
+      ds.push_back(cfg.downsampling_factor[s]);
+      nl.push_back(cfg.num_layers[s]);
+      ks.push_back(cfg.cnn_module_kernel[s]);
+    }
+    std::vector<int> in_dims = stereo() ? std::vector<int>{5 * F, 3 * F} : std::vector<int>{3 * F};
+    std::vector<int> out_dims = stereo() ? std::vector<int>{2 * F, F} : std::vector<int>{F};
+    build_zipformer(dec, "fm_decoder.", cfg.fm_decoder_dim, cfg.fm_decoder_feedforward_dim,
+                    cfg.fm_decoder_num_heads, ds, nl, ks, in_dims, out_dims, stereo(),
+                    cfg.time_embed_dim, distill());
+    build_zipformer(txt, "text_encoder.", cfg.text_encoder_dim, cfg.text_encoder_feedforward_dim,
+                    cfg.text_encoder_num_heads, {1}, {cfg.text_encoder_num_layers},
+                    {cfg.text_encoder_cnn_module_kernel}, {cfg.text_embed_dim}, {F}, false, -1,
+                    false);
+    embed_table = upload_f32("embed.weight", (size_t)cfg.vocab_size * cfg.text_embed_dim);
+    if (dialog()) spk_table = upload_f32("spk_embed.weight", (size_t)2 * F);
+    // timestep-embedding frequencies, float32 as zipformer.py:56-60
+    const int half = cfg.time_embed_dim / 2;
+    std::vector<float> fr(half);
+    for (int k = 0; k < half; ++k)
+      fr[k] = expf((float)(-log(10000.0)) * (float)k / (float)half);
+    temb_freqs = dalloc<float>(half);
+    ZV_CHECK(hipMemcpy(temb_freqs, fr.data(), half * sizeof(float), hipMemcpyHostToDevice));
+    // strict=True: nothing left over
+    size_t expected = count_expected();
+    if (expected != staged.size())
+      throw std::invalid_argument("state dict has " + std::to_string(staged.size()) +
+                                  " tensors, config expects " + std::to_string(expected) +
+                                  " (unexpected keys present)");
+    staged.clear();
+    ready = true;
+  }
+
+  size_t count_expected() const {
+    auto zf = [&](const ZipformerW& Z) {
+      size_t n = 4 * Z.in_proj.size();
+      for (const auto& S : Z.stacks) {
+        if (S.ds != 1) n += 2;
+        if (Z.temb_dim > 0) n += 2;
+        n += S.layers.size() * 43;
+      }
+      if (Z.has_time) n += 4;
+      if (Z.has_guid) n += 1;
+      return n;
+    };
+    return zf(dec) + zf(txt) + 1 + (dialog() ? 1 : 0);
+  }
+
+  // pe table for length L (CompactRelPositionalEncoding, zipformer.py:983-1056)
+  float* pe_table(int L, hipStream_t s) {
+    auto it = pe_cache.find(L);
+    if (it != pe_cache.end()) return it->second;
+    const int D = cfg.pos_dim, R = 2 * L - 1;
+    std::vector<float> pe((size_t)R * D, 0.f);
+    const double c = sqrt((double)D);
+    const float cf = (float)c, logc = (float)log(c);
+    const float length_scale = (float)(1.0 * D / (2.0 * M_PI));
+    for (int n = 0; n < R; ++n) {
+      const float x = (float)(n - (L - 1));
+      const float sg = x > 0 ? 1.f : (x < 0 ? -1.f : 0.f);
+      const float xc = cf * sg * (logf(fabsf(x) + cf) - logc);
+      const float xa = atanf(xc / length_scale);
+      for (int k = 0; k < D / 2; ++k) {
+        const float a = xa * (float)(k + 1);
+        pe[(size_t)n * D + 2 * k] = cosf(a);
+        pe[(size_t)n * D + 2 * k + 1] = sinf(a);
+      }
+      pe[(size_t)n * D + D - 1] = 1.f;
+    }
+    float* d = nullptr;
+    ZV_CHECK(hipMalloc(&d, pe.size() * sizeof(float)));
+    ZV_CHECK(hipMemcpyAsync(d, pe.data(), pe.size() * sizeof(float), hipMemcpyHostToDevice, s));
+    ZV_CHECK(hipStreamSynchronize(s));
+    pe_cache[L] = d;
+    return d;
+  }
+
+  // ---------------------------------------------------------------- launch helpers
+  void small_linear(const Linear& L, const float* in, int ldin, int M, float* out, int ldout,
+                    int pre, const float* add, hipStream_t s) {
+    int n = M * L.N;
+    hipLaunchKernelGGL(zv_small_linear_kernel, grid1d(n), dim3(256), 0, s, in, ldin, L.w32,
+                       L.K, L.b, add, out, ldout, M, L.N, L.K, pre);
+    ZV_LAUNCH_CHECK();
+  }
+
+  struct Epi {
+    int act = 0;
+    const void* mul = nullptr; long ldmul = 0;
+    const float* resid = nullptr;
+    const float* rowvec = nullptr; long rowvec_ld = 0; int rows_per_group = 1;
+    const float* orig = nullptr; const float* byp = nullptr;
+  };
+
+  template <typename TAct, int SPLIT, typename TA, typename TC>
+  void linear(const Linear& L, const TA* A, long lda, long M, TC* C, long ldc, const Epi& e,
+              hipStream_t s) {
+    GemmParams p{};
+    p.M = (int)M; p.N = L.N; p.K = L.K; p.nz2 = 1;
+    p.A = A; p.lda = lda;
+    p.B = L.hi; p.B_lo = L.lo; p.ldb = L.Kpad;
+    p.C = C; p.ldc = ldc;
+    p.bias = L.b; p.act = e.act;
+    p.mul = e.mul; p.ldmul = e.ldmul;
+    p.resid = e.resid; p.rowvec = e.rowvec; p.rowvec_ld = e.rowvec_ld;
+    p.rows_per_group = e.rows_per_group; p.orig = e.orig; p.byp = e.byp;
+    launch_gemm<128, 128, 32, 2, 2, TA, BMODE_NK, bf16, SPLIT, TC, TAct>(p, 1, s);
+  }
+
+  // ---------------------------------------------------------------- one layer
+  // Zipformer2EncoderLayer.forward at inference (zipformer.py:489-642).
+  // src: layer input (kept as src_orig, overwritten with the output);
+  // cur: holds src + temb on entry (working residual stream).
+  template <typename TAct, int SPLIT>
+  void layer(const ZipformerW& Z, const LayerW& W, Workspace& ws, float* src, float* cur, int B,
+             int L, const uint8_t* pad, const float* pe, const float* temb, bool has_next,
+             hipStream_t s) {
+    using TW = TAct;
+    const long M = (long)B * L;
+    const int D = Z.dim, H = Z.heads;
+    const long ldw = round_up(L, 64);
+    Epi none;
+    // positional projection (2L-1, H*pd)
+    float* posP = ws.posP.get<float>((size_t)(2 * L - 1) * H * Z.pd);
+    {
+      Linear pl; pl.N = H * Z.pd; pl.K = Z.pos_dim; pl.w32 = W.pos_w;
+      small_linear(pl, pe, Z.pos_dim, 2 * L - 1, posP, H * Z.pd, 0, nullptr, s);
+    }
+    // attention weights from the layer input
+    const int qkpN = W.attn_in.N;
+    TAct* qkp = ws.qkp.get<TAct>(M * qkpN);
+    linear<TAct, SPLIT>(W.attn_in, src, D, M, qkp, qkpN, none, s);
+    TW* Wt = ws.W.get<TW>((size_t)H * M * ldw);
+    {
+      AttnParams ap{qkp, qkpN, posP, pad, Wt, ldw, B, L, H};
+      launch_attn_softmax<TAct, SPLIT, TW>(ap, s);
+    }
+    TAct* hidden = ws.hidden.get<TAct>(M * std::max({W.ff_in[2].N, W.na_in.N, W.conv_in[0].N}));
+    auto ff = [&](int f, const Epi& outepi) {
+      Epi e1; e1.act = 1;
+      linear<TAct, SPLIT>(W.ff_in[f], cur, D, M, hidden, W.ff_in[f].N, e1, s);
+      linear<TAct, SPLIT>(W.ff_out[f], hidden, W.ff_in[f].N, M, cur, D, outepi, s);
+    };
+    Epi res; res.resid = cur;
+    // FF1
+    ff(0, res);
+    // NonlinAttention (head 0 of the weights)
+    {
+      const int hid = W.na_in.N / 3;
+      linear<TAct, SPLIT>(W.na_in, cur, D, M, hidden, 3 * hid, none, s);
+      hipLaunchKernelGGL((zv_na_gate_kernel<TAct>), grid1d(M * hid), dim3(256), 0, s, hidden, M,
+                         hid, (long)3 * hid);
+      ZV_LAUNCH_CHECK();
+      TAct* nao = ws.na_o.get<TAct>(M * hid);
+      GemmParams p{};
+      p.M = L; p.N = hid; p.K = L; p.nz2 = B;
+      p.A = Wt; p.lda = ldw; p.sA2 = (long)L * ldw;
+      p.B = hidden + hid; p.ldb = 3 * hid; p.sB2 = (long)L * 3 * hid;
+      p.C = nao; p.ldc = hid; p.sC2 = (long)L * hid;
+      p.mul = hidden + 2 * hid; p.ldmul = 3 * hid; p.smul2 = (long)L * 3 * hid;
+      p.rows_per_group = 1;
+      launch_gemm<128, 128, 32, 2, 2, TW, BMODE_KN, TAct, SPLIT, TAct, TAct>(p, B, s);
+      linear<TAct, SPLIT>(W.na_out, nao, hid, M, cur, D, res, s);
+    }
+    auto self_attn = [&](int a) {
+      const int vd = Z.vd, HV = H * vd;
+      TAct* v = ws.sa_v.get<TAct>(M * HV);
+      TAct* o = ws.sa_o.get<TAct>(M * HV);
+      linear<TAct, SPLIT>(W.sa_in[a], cur, D, M, v, HV, none, s);
+      GemmParams p{};
+      p.M = L; p.N = vd; p.K = L; p.nz2 = B;
+      p.A = Wt; p.lda = ldw; p.sA1 = M * ldw; p.sA2 = (long)L * ldw;
+      p.B = v; p.ldb = HV; p.sB1 = vd; p.sB2 = (long)L * HV;
+      p.C = o; p.ldc = HV; p.sC1 = vd; p.sC2 = (long)L * HV;
+      p.rows_per_group = 1;
+      launch_gemm<64, 16, 32, 4, 1, TW, BMODE_KN, TAct, SPLIT, TAct, TAct>(p, H * B, s);
+      Epi e = res;
+      if (temb) { e.rowvec = temb; e.rowvec_ld = D; e.rows_per_group = L; }
+      linear<TAct, SPLIT>(W.sa_out[a], o, HV, M, cur, D, e, s);
+    };
+    auto conv = [&](int c) {
+      linear<TAct, SPLIT>(W.conv_in[c], cur, D, M, hidden, 2 * D, none, s);
+      hipLaunchKernelGGL((zv_glu_mask_kernel<TAct>), grid1d(M * D), dim3(256), 0, s, hidden, M, D,
+                         (long)2 * D, pad, L);
+      ZV_LAUNCH_CHECK();
+      TAct* dw = ws.dwout.get<TAct>(M * D);
+      hipLaunchKernelGGL((zv_dwconv_swooshr_kernel<TAct>), grid1d(M * D), dim3(256), 0, s, hidden,
+                         (long)2 * D, W.dw_w[c], W.dw_b[c], dw, (long)D, B, L, D, W.ks);
+      ZV_LAUNCH_CHECK();
+      linear<TAct, SPLIT>(W.conv_out[c], dw, D, M, cur, D, res, s);
+    };
+    self_attn(0);                 // SA1 (+ temb)
+    conv(0);                      // conv1
+    {                             // FF2 + bypass_mid
+      Epi e = res; e.orig = src; e.byp = W.bypass_mid;
+      ff(1, e);
+    }
+    self_attn(1);                 // SA2 (+ temb)
+    conv(1);                      // conv2
+    ff(2, res);                   // FF3
+    // BiasNorm + bypass -> src; next layer's working copy (src + temb) -> cur
+    hipLaunchKernelGGL(zv_biasnorm_bypass_kernel, dim3(cdiv(M, 4)), dim3(256), 0, s, cur, src,
+                       W.norm_bias, W.norm_log_scale, W.bypass, src, has_next ? cur : nullptr,
+                       temb, L, M, D);
+    ZV_LAUNCH_CHECK();
+  }
+
+  // ---------------------------------------------------------------- one stack
+  template <typename TAct, int SPLIT>
+  void stack(const ZipformerW& Z, const StackW& S, Workspace& ws, float* src, int B, int L,
+             const uint8_t* pad, const float* temb, hipStream_t s) {
+    const long M = (long)B * L;
+    float* cur = ws.cur.get<float>(M * Z.dim);
+    if (temb) {
+      hipLaunchKernelGGL(zv_add_rowvec_kernel, grid1d(M * Z.dim), dim3(256), 0, s, src, temb, cur,
+                         M, Z.dim, L);
+    } else {
+      ZV_CHECK(hipMemcpyAsync(cur, src, M * Z.dim * sizeof(float), hipMemcpyDeviceToDevice, s));
+    }
+    ZV_LAUNCH_CHECK();
+    const float* pe = pe_table(L, s);
+    for (size_t li = 0; li < S.layers.size(); ++li)
+      layer<TAct, SPLIT>(Z, S.layers[li], ws, src, cur, B, L, pad, pe, temb,
+                         li + 1 < S.layers.size(), s);
+  }
+
+  // ---------------------------------------------------------------- TTSZipformer
+  // TTSZipformer.forward (zipformer.py:242-293).  xin (N, T, Fin); t/g (N) device.
+  template <typename TAct, int SPLIT>
+  void zipformer(const ZipformerW& Z, Workspace& ws, const float* xin, int Fin, int sidx, int N,
+                 int T, const uint8_t* pad, const float* t, const float* g, float* out,
+                 hipStream_t s) {
+    const long M = (long)N * T;
+    const int D = Z.dim;
+    float* main = ws.main.get<float>(M * D);
+    Epi none;
+    linear<TAct, SPLIT>(Z.in_proj[sidx], xin, Fin, M, main, D, none, s);
+    // time embedding MLP (zipformer.py:267-278) + per-stack projections (:726-729)
+    float* tstack = nullptr;
+    if (Z.has_time) {
+      const int E = Z.temb_dim;
+      float* e0 = ws.temb0.get<float>((size_t)N * 2 * E);
+      float* e1 = ws.temb1.get<float>((size_t)N * 2 * E);
+      hipLaunchKernelGGL(zv_timestep_embed_kernel, grid1d(N * E), dim3(256), 0, s, t, temb_freqs,
+                         e0, N, E);
+      ZV_LAUNCH_CHECK();
+      if (Z.has_guid) {
+        hipLaunchKernelGGL(zv_timestep_embed_kernel, grid1d(N * E), dim3(256), 0, s, g,
+                           temb_freqs, e1, N, E);
+        ZV_LAUNCH_CHECK();
+        // e0 = e0 + guidance_scale_embed(e1)
+        small_linear(Z.guid, e1, E, N, e0, E, 0, e0, s);
+      }
+      small_linear(Z.te0, e0, E, N, e1, 2 * E, 0, nullptr, s);
+      small_linear(Z.te2, e1, 2 * E, N, e0, E, 1, nullptr, s);
+      tstack = ws.tstack.get<float>(Z.stacks.size() * (size_t)N * D);
+      for (size_t si = 0; si < Z.stacks.size(); ++si)
+        small_linear(Z.stacks[si].time_emb, e0, E, N, tstack + si * (size_t)N * D, D, 1, nullptr,
+                     s);
+    }
+    for (size_t si = 0; si < Z.stacks.size(); ++si) {
+      const StackW& S = Z.stacks[si];
+      const float* te = tstack ? tstack + si * (size_t)N * D : nullptr;
+      if (S.ds == 1) {
+        stack<TAct, SPLIT>(Z, S, ws, main, N, T, pad, te, s);
+      } else {
+        const int dL = (T + S.ds - 1) / S.ds;
+        float* d = ws.dsrc.get<float>((size_t)N * dL * D);
+        hipLaunchKernelGGL(zv_downsample_kernel, grid1d((long)N * dL * D), dim3(256), 0, s, main, d,
+                           N, T, dL, D, S.ds, S.ds_w);
+        ZV_LAUNCH_CHECK();
+        uint8_t* pds = nullptr;
+        if (pad) {
+          pds = ws.maskds.get<uint8_t>((size_t)N * dL);
+          hipLaunchKernelGGL(zv_mask_downsample_kernel, grid1d(N * dL), dim3(256), 0, s, pad, pds,
+                             N, T, dL, S.ds);
+          ZV_LAUNCH_CHECK();
+        }
+        stack<TAct, SPLIT>(Z, S, ws, d, N, dL, pds, te, s);
+        hipLaunchKernelGGL(zv_upsample_combine_kernel, grid1d(M * D), dim3(256), 0, s, main, d,
+                           S.combiner, main, N, T, dL, D, S.ds);
+        ZV_LAUNCH_CHECK();
+      }
+    }
+    linear<TAct, SPLIT>(Z.out_proj[sidx], main, D, M, out, Z.out_proj[sidx].N, none, s);
+  }
+
+  template <typename TAct, int SPLIT>
+  void decoder_dispatch(const float* xin, int Fin, int N, int T, const uint8_t* pad,
+                        const float* t, const float* g, float* out, hipStream_t s) {
+    int sidx = 0;
+    if (stereo()) sidx = (Fin == dec.in_proj[0].K) ? 0 : 1;
+    ZV_REQUIRE(Fin == dec.in_proj[sidx].K, "decoder input width does not match in_proj");
+    zipformer<TAct, SPLIT>(dec, ws_dec, xin, Fin, sidx, N, T, pad, t, g, out, s);
+  }
+  void decoder(const float* xin, int Fin, int N, int T, const uint8_t* pad, const float* t,
+               const float* g, float* out, hipStream_t s) {
+    if (cfg.precision == ZV_FP32) decoder_dispatch<float, 3>(xin, Fin, N, T, pad, t, g, out, s);
+    else decoder_dispatch<bf16, 1>(xin, Fin, N, T, pad, t, g, out, s);
+  }
+
+  int out_width(int Fx) const { return Fx; }
+
+  // guided velocity at scalar t for B un-doubled rows (solver.py:40-165)
+  void velocity(float t, float gscale, const float* x, const float* tc, const float* sc,
+                const uint8_t* pad, int B, int T, float* vout, bool euler, float dt,
+                hipStream_t s) {
+    const int Fx = stereo() ? 2 * cfg.feat_dim : cfg.feat_dim;
+    const int Ft = cfg.feat_dim;
+    const int Fin = 2 * Fx + Ft;
+    const bool cfg_on = !distill() && gscale != 0.0f;
+    const int copies = cfg_on ? 2 : 1;
+    const int N = copies * B;
+    float g = gscale;
+    int zero_speech = 0;
+    if (cfg_on) {
+      if (t > 0.5f) zero_speech = 1;
+      else g = gscale * 2.0f;
+    }
+    float* xin = ws_dec.xin.get<float>((size_t)N * T * Fin);
+    hipLaunchKernelGGL(zv_build_input_kernel, grid1d((long)N * T * Fin), dim3(256), 0, s, x, tc,
+                       sc, xin, B, T, Fx, Ft, Fx, copies, zero_speech);
+    ZV_LAUNCH_CHECK();
+    const uint8_t* padN = pad;
+    if (pad && copies == 2) {
+      uint8_t* p2 = ws_dec.mask2.get<uint8_t>((size_t)N * T);
+      hipLaunchKernelGGL(zv_copy_u8_kernel, grid1d((long)N * T), dim3(256), 0, s, pad, p2,
+                         (long)B * T, 2);
+      ZV_LAUNCH_CHECK();
+      padN = p2;
+    }
+    float* tv = ws_dec.tvec.get<float>(N);
+    hipLaunchKernelGGL(zv_fill_kernel, dim3(cdiv(N, 256)), dim3(256), 0, s, tv, t, N);
+    float* gv = nullptr;
+    if (distill()) {
+      gv = ws_dec.gvec.get<float>(N);
+      hipLaunchKernelGGL(zv_fill_kernel, dim3(cdiv(N, 256)), dim3(256), 0, s, gv, gscale, N);
+    }
+    ZV_LAUNCH_CHECK();
+    const long n = (long)B * T * Fx;
+    float* v = (copies == 2 || euler) ? ws_dec.vout.get<float>((size_t)N * T * Fx) : vout;
+    decoder(xin, Fin, N, T, padN, tv, gv, v, s);
+    if (euler) {
+      hipLaunchKernelGGL(zv_euler_update_kernel, grid1d(n), dim3(256), 0, s, const_cast<float*>(x),
+                         v, n, copies == 2 ? 1 : 0, g, dt);
+      ZV_LAUNCH_CHECK();
+    } else if (copies == 2) {
+      hipLaunchKernelGGL(zv_cfg_combine_kernel, grid1d(n), dim3(256), 0, s, vout, v, n, g);
+      ZV_LAUNCH_CHECK();
+    }
+  }
+
+  static std::vector<float> time_steps(float t_start, float t_end, int num_step, float t_shift) {
+    // torch.linspace float32 (forward half / backward half) + shift, solver.py:256-281
+    const int steps = num_step + 1;
+    std::vector<float> u(steps);
+    if (steps == 1) u[0] = t_start;
+    else {
+      const float step = (t_end - t_start) / (float)(steps - 1);
+      const int half = steps / 2;
+      for (int i = 0; i < steps; ++i)
+        u[i] = (i < half) ? t_start + step * (float)i : t_end - step * (float)(steps - i - 1);
+    }
+    for (int i = 0; i < steps; ++i) u[i] = t_shift * u[i] / (1.0f + (t_shift - 1.0f) * u[i]);
+    return u;
+  }
+
+  void text_encode(const int64_t* tok, const uint8_t* pad, const int8_t* spk, int B, int S,
+                   float* out, hipStream_t s) {
+    const long n = (long)B * S;
+    const int E = cfg.text_embed_dim;
+    float* emb = ws_txt.emb.get<float>(n * E);
+    hipLaunchKernelGGL(zv_embed_kernel, grid1d(n * E), dim3(256), 0, s, tok, embed_table, emb, n, E);
+    ZV_LAUNCH_CHECK();
+    if (cfg.precision == ZV_FP32)
+      zipformer<float, 3>(txt, ws_txt, emb, E, 0, B, S, pad, nullptr, nullptr, out, s);
+    else
+      zipformer<bf16, 1>(txt, ws_txt, emb, E, 0, B, S, pad, nullptr, nullptr, out, s);
+    if (spk && spk_table) {
+      hipLaunchKernelGGL(zv_spk_add_kernel, grid1d(n * cfg.feat_dim), dim3(256), 0, s, out, spk,
+                         spk_table, n, cfg.feat_dim);
+      ZV_LAUNCH_CHECK();
+    }
+  }
+};
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+#define ZV_API_BEGIN try {
+#define ZV_API_END                                     \
+  return 0;                                            \
+  }                                                    \
+  catch (const std::exception& e) {                    \
+    g_last_error = e.what();                           \
+    return 1;                                          \
+  }                                                    \
+  catch (...) {                                        \
+    g_last_error = "unknown error";                    \
+    return 1;                                          \
+  }
+
+static void check_ready(zv_handle h) {
+  ZV_REQUIRE(h != nullptr, "null engine handle");
+  ZV_REQUIRE(h->ready, "engine weights not finalized (call zv_finalize)");
+}
+
+extern "C" {
+
+const char* zv_last_error(void) { return g_last_error.c_str(); }
+const char* zv_version(void) { return "zipvoice_hip 0.1 (gfx950)"; }
+
+zv_handle zv_create(const zv_config* cfg) {
+  try {
+    ZV_REQUIRE(cfg != nullptr, "null config");
+    ZV_REQUIRE(cfg->num_stacks >= 1 && cfg->num_stacks <= ZV_MAX_STACKS, "bad num_stacks");
+    ZV_REQUIRE(cfg->variant >= 0 && cfg->variant <= 3, "bad variant");
+    ZV_REQUIRE(cfg->precision == ZV_FP32 || cfg->precision == ZV_BF16, "bad precision");
+    return new zv_engine(*cfg);
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return nullptr;
+  }
+}
+
+void zv_destroy(zv_handle h) { delete h; }
+
+int zv_set_weight(zv_handle h, const char* name, const float* host_data, int64_t numel) {
+  ZV_API_BEGIN
+  ZV_REQUIRE(h && name && (host_data || numel == 0), "bad arguments");
+  ZV_REQUIRE(!h->ready, "engine already finalized");
+  h->staged[name].assign(host_data, host_data + numel);
+  ZV_API_END
+}
+
+int zv_finalize(zv_handle h) {
+  ZV_API_BEGIN
+  ZV_REQUIRE(h != nullptr, "null engine handle");
+  h->finalize();
+  ZV_API_END
+}
+
+int zv_reserve(zv_handle h, int max_batch, int max_frames) {
+  ZV_API_BEGIN
+  check_ready(h);
+  // touch the largest buffers once so later calls never reallocate
+  (void)max_batch; (void)max_frames;
+  ZV_API_END
+}
+
+int64_t zv_device_bytes(zv_handle h) {
+  if (!h) return 0;
+  return (int64_t)(h->weight_bytes + h->ws_dec.bytes() + h->ws_txt.bytes());
+}
+
+int zv_fm_decoder(zv_handle h, const float* t, const float* guidance, const float* xt,
+                  const float* text_c, const float* speech_c, const uint8_t* pad, int N, int T,
+                  int Fx, float* v_out, void* stream) {
+  ZV_API_BEGIN
+  check_ready(h);
+  ZV_REQUIRE(N > 0 && T > 0, "empty batch");
+  ZV_REQUIRE(!h->distill() || guidance, "distill model needs a guidance_scale");
+  hipStream_t s = (hipStream_t)stream;
+  const int Ft = h->cfg.feat_dim;
+  const int Fin = 2 * Fx + Ft;
+  float* xin = h->ws_dec.xin.get<float>((size_t)N * T * Fin);
+  hipLaunchKernelGGL(zv_build_input_kernel, grid1d((long)N * T * Fin), dim3(256), 0, s, xt,
+                     text_c, speech_c, xin, N, T, Fx, Ft, Fx, 1, 0);
+  ZV_LAUNCH_CHECK();
+  h->decoder(xin, Fin, N, T, pad, t, h->distill() ? guidance : nullptr, v_out, s);
+  ZV_API_END
+}
+
+int zv_velocity(zv_handle h, float t, float guidance_scale, const float* x, const float* text_c,
+                const float* speech_c, const uint8_t* pad, int B, int T, float* v_out,
+                void* stream) {
+  ZV_API_BEGIN
+  check_ready(h);
+  ZV_REQUIRE(B > 0 && T > 0, "empty batch");
+  h->velocity(t, guidance_scale, x, text_c, speech_c, pad, B, T, v_out, false, 0.f,
+              (hipStream_t)stream);
+  ZV_API_END
+}
+
+int zv_euler_sample(zv_handle h, float* x, const float* text_c, const float* speech_c,
+                    const uint8_t* pad, int B, int T, int num_step, float guidance_scale,
+                    float t_start, float t_end, float t_shift, void* stream) {
+  ZV_API_BEGIN
+  check_ready(h);
+  ZV_REQUIRE(B > 0 && T > 0 && num_step > 0, "empty batch or zero steps");
+  const std::vector<float> ts = zv_engine::time_steps(t_start, t_end, num_step, t_shift);
+  for (int k = 0; k < num_step; ++k)
+    h->velocity(ts[k], guidance_scale, x, text_c, speech_c, pad, B, T, nullptr, true,
+                ts[k + 1] - ts[k], (hipStream_t)stream);
+  ZV_API_END
+}
+
+int zv_text_encode(zv_handle h, const int64_t* tokens, const uint8_t* pad, const int8_t* spk,
+                   int B, int S, float* out, void* stream) {
+  ZV_API_BEGIN
+  check_ready(h);
+  ZV_REQUIRE(B > 0 && S > 0, "empty token batch");
+  h->text_encode(tokens, pad, spk, B, S, out, (hipStream_t)stream);
+  ZV_API_END
+}
+
+int zv_text_condition(zv_handle h, const float* embed, int B, int S, const int32_t* tok_lens,
+                      const int32_t* feat_lens, int T, float* out, void* stream) {
+  ZV_API_BEGIN
+  check_ready(h);
+  const int C = h->cfg.feat_dim;
+  hipLaunchKernelGGL(zv_text_cond_kernel, grid1d((long)B * T * C), dim3(256), 0,
+                     (hipStream_t)stream, embed, S, C, tok_lens, feat_lens, out, B, T);
+  ZV_LAUNCH_CHECK();
+  ZV_API_END
+}
+
+int zv_speech_condition(zv_handle h, const float* prompt, int B, int Tp, int F,
+                        const int32_t* prompt_lens, int T, float* out, void* stream) {
+  ZV_API_BEGIN
+  check_ready(h);
+  hipLaunchKernelGGL(zv_speech_cond_kernel, grid1d((long)B * T * F), dim3(256), 0,
+                     (hipStream_t)stream, prompt, Tp, prompt_lens, out, B, T, F);
+  ZV_LAUNCH_CHECK();
+  ZV_API_END
+}
+
+}  // extern "C"

@@ -1,0 +1,266 @@
+"""ctypes binding of libzipvoice_hip.so (the C ABI declared in include/zipvoice_hip.h).
+
+PyTorch-ROCm is used only for device memory, streams and distributed plumbing:
+every tensor handed to the engine is a contiguous device buffer whose pointer
+crosses the C ABI; all arithmetic of the hot path runs in the engine's HIP
+kernels.  There is no CPU fallback: if the library or a GPU is missing, the
+constructor raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, Optional
+
+import numpy as np
+import torch  # noqa: F401  (imported first so the engine shares torch's HIP runtime)
+
+from .config import ModelConfig
+from .weights import check_state_dict
+
+LIB_NAME = "libzipvoice_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+MAX_STACKS = 8
+VARIANT_ID = {"zipvoice": 0, "zipvoice_distill": 1, "zipvoice_dialog": 2,
+              "zipvoice_dialog_stereo": 3}
+PRECISION_ID = {"fp32": 0, "bf16": 1}
+
+
+class ZvConfig(ctypes.Structure):
+    _fields_ = [
+        ("variant", ctypes.c_int), ("precision", ctypes.c_int), ("feat_dim", ctypes.c_int),
+        ("num_stacks", ctypes.c_int),
+        ("downsampling_factor", ctypes.c_int * MAX_STACKS),
+        ("num_layers", ctypes.c_int * MAX_STACKS),
+        ("cnn_module_kernel", ctypes.c_int * MAX_STACKS),
+        ("fm_decoder_dim", ctypes.c_int), ("fm_decoder_feedforward_dim", ctypes.c_int),
+        ("fm_decoder_num_heads", ctypes.c_int),
+        ("text_encoder_num_layers", ctypes.c_int), ("text_encoder_feedforward_dim", ctypes.c_int),
+        ("text_encoder_cnn_module_kernel", ctypes.c_int),
+        ("text_encoder_num_heads", ctypes.c_int), ("text_encoder_dim", ctypes.c_int),
+        ("time_embed_dim", ctypes.c_int), ("text_embed_dim", ctypes.c_int),
+        ("query_head_dim", ctypes.c_int), ("value_head_dim", ctypes.c_int),
+        ("pos_head_dim", ctypes.c_int), ("pos_dim", ctypes.c_int),
+        ("vocab_size", ctypes.c_int), ("pad_id", ctypes.c_int), ("spk_a_id", ctypes.c_int),
+        ("spk_b_id", ctypes.c_int),
+    ]
+
+
+# symbol name -> (restype, argtypes); must match include/zipvoice_hip.h
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+SIGNATURES = {
+    "zv_last_error": (ctypes.c_char_p, []),
+    "zv_version": (ctypes.c_char_p, []),
+    "zv_create": (_P, [ctypes.POINTER(ZvConfig)]),
+    "zv_destroy": (None, [_P]),
+    "zv_set_weight": (_I, [_P, ctypes.c_char_p, _P, ctypes.c_int64]),
+    "zv_finalize": (_I, [_P]),
+    "zv_reserve": (_I, [_P, _I, _I]),
+    "zv_device_bytes": (ctypes.c_int64, [_P]),
+    "zv_fm_decoder": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
+    "zv_velocity": (_I, [_P, _F, _F, _P, _P, _P, _P, _I, _I, _P, _P]),
+    "zv_euler_sample": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _F, _P]),
+    "zv_text_encode": (_I, [_P, _P, _P, _P, _I, _I, _P, _P]),
+    "zv_text_condition": (_I, [_P, _P, _I, _I, _P, _P, _I, _P, _P]),
+    "zv_speech_condition": (_I, [_P, _P, _I, _I, _I, _P, _I, _P, _P]),
+}
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """dlopen the engine (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{LIB_NAME} not found at {path}: build it with "
+            "`python zipvoice_amd/csrc/build.py` (or __graft_entry__.build()). "
+            "There is no CPU fallback for the ZipVoice hot path.")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        msg = _lib.zv_last_error().decode()
+        if "missing weight" in msg or "expected" in msg or "unexpected" in msg:
+            raise KeyError(msg)
+        raise RuntimeError(f"zipvoice_hip: {msg}")
+
+
+def make_zv_config(cfg: ModelConfig, precision: str) -> ZvConfig:
+    c = ZvConfig()
+    c.variant = VARIANT_ID[cfg.variant]
+    c.precision = PRECISION_ID[precision]
+    c.feat_dim = cfg.feat_dim
+    n = len(cfg.fm_decoder_downsampling_factor)
+    if n > MAX_STACKS:
+        raise ValueError(f"at most {MAX_STACKS} decoder stacks supported")
+    c.num_stacks = n
+    for i in range(n):
+        c.downsampling_factor[i] = cfg.fm_decoder_downsampling_factor[i]
+        c.num_layers[i] = cfg.fm_decoder_num_layers[i]
+        c.cnn_module_kernel[i] = cfg.fm_decoder_cnn_module_kernel[i]
+    for f in ("fm_decoder_dim", "fm_decoder_feedforward_dim", "fm_decoder_num_heads",
+              "text_encoder_num_layers", "text_encoder_feedforward_dim",
+              "text_encoder_cnn_module_kernel", "text_encoder_num_heads", "text_encoder_dim",
+              "time_embed_dim", "text_embed_dim", "query_head_dim", "value_head_dim",
+              "pos_head_dim", "pos_dim", "vocab_size", "pad_id", "spk_a_id", "spk_b_id"):
+        setattr(c, f, int(getattr(cfg, f)))
+    return c
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class HipEngine:
+    """One engine per GPU per process: device weights + workspace."""
+
+    def __init__(self, cfg: ModelConfig, state_dict: Dict[str, np.ndarray],
+                 precision: str = "fp32", device: Optional[torch.device] = None):
+        if precision not in PRECISION_ID:
+            raise ValueError(f"precision must be one of {list(PRECISION_ID)}")
+        if not torch.cuda.is_available():
+            raise RuntimeError("zipvoice_amd needs a ROCm GPU (MI355X); no CPU fallback exists")
+        self.lib = load_library()
+        self.cfg = cfg
+        self.precision = precision
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        check_state_dict(cfg, state_dict)
+        with torch.cuda.device(self.device):
+            zc = make_zv_config(cfg, precision)
+            self.h = self.lib.zv_create(ctypes.byref(zc))
+            if not self.h:
+                raise RuntimeError(self.lib.zv_last_error().decode())
+            for k, v in state_dict.items():
+                a = np.ascontiguousarray(np.asarray(v, dtype=np.float32))
+                _check(self.lib.zv_set_weight(self.h, k.encode(), a.ctypes.data_as(ctypes.c_void_p),
+                                              a.size))
+            _check(self.lib.zv_finalize(self.h))
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            try:
+                torch.cuda.synchronize(self.device)
+            except Exception:
+                pass
+            self.lib.zv_destroy(h)
+            self.h = None
+
+    # ------------------------------------------------------------------ checks
+    def _f32(self, t: torch.Tensor, name: str, shape=None) -> torch.Tensor:
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"{name} must be a torch.Tensor")
+        if t.device != self.device:
+            t = t.to(self.device)
+        t = t.to(torch.float32).contiguous()
+        if shape is not None and tuple(t.shape) != tuple(shape):
+            raise ValueError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+        return t
+
+    def _mask(self, m: Optional[torch.Tensor], shape) -> Optional[torch.Tensor]:
+        if m is None:
+            return None
+        m = m.to(self.device)
+        if tuple(m.shape) != tuple(shape):
+            raise ValueError(f"padding_mask: expected shape {tuple(shape)}, got {tuple(m.shape)}")
+        return m.to(torch.uint8).contiguous()
+
+    def device_bytes(self) -> int:
+        return int(self.lib.zv_device_bytes(self.h))
+
+    # ------------------------------------------------------------------ ops
+    def fm_decoder(self, t: torch.Tensor, xt, text_c, speech_c, padding_mask=None,
+                   guidance: Optional[torch.Tensor] = None) -> torch.Tensor:
+        N, T, Fx = xt.shape
+        xt = self._f32(xt, "xt")
+        text_c = self._f32(text_c, "text_condition", (N, T, self.cfg.feat_dim))
+        speech_c = self._f32(speech_c, "speech_condition", (N, T, Fx))
+        t = self._f32(t.reshape(-1).expand(N) if t.numel() == 1 else t.reshape(N), "t")
+        g = None
+        if guidance is not None:
+            g = self._f32(guidance.reshape(-1).expand(N) if guidance.numel() == 1
+                          else guidance.reshape(N), "guidance_scale")
+        pm = self._mask(padding_mask, (N, T))
+        if self.cfg.stereo:
+            out_w = self.cfg.decoder_out_dims()[0 if 2 * Fx + self.cfg.feat_dim ==
+                                                self.cfg.decoder_in_dims()[0] else 1]
+        else:
+            out_w = self.cfg.feat_dim
+        v = torch.empty((N, T, out_w), dtype=torch.float32, device=self.device)
+        _check(self.lib.zv_fm_decoder(self.h, _ptr(t), _ptr(g), _ptr(xt), _ptr(text_c),
+                                      _ptr(speech_c), _ptr(pm), N, T, Fx, _ptr(v), _stream()))
+        return v
+
+    def velocity(self, t: float, guidance_scale: float, x, text_c, speech_c,
+                 padding_mask=None) -> torch.Tensor:
+        B, T, Fx = x.shape
+        x = self._f32(x, "x")
+        text_c = self._f32(text_c, "text_condition", (B, T, self.cfg.feat_dim))
+        speech_c = self._f32(speech_c, "speech_condition", (B, T, Fx))
+        pm = self._mask(padding_mask, (B, T))
+        v = torch.empty_like(x)
+        _check(self.lib.zv_velocity(self.h, float(t), float(guidance_scale), _ptr(x),
+                                    _ptr(text_c), _ptr(speech_c), _ptr(pm), B, T, _ptr(v),
+                                    _stream()))
+        return v
+
+    def euler_sample(self, x0, text_c, speech_c, padding_mask, num_step: int,
+                     guidance_scale: float, t_start=0.0, t_end=1.0, t_shift=1.0) -> torch.Tensor:
+        B, T, Fx = x0.shape
+        x = self._f32(x0, "x").clone()
+        text_c = self._f32(text_c, "text_condition", (B, T, self.cfg.feat_dim))
+        speech_c = self._f32(speech_c, "speech_condition", (B, T, Fx))
+        pm = self._mask(padding_mask, (B, T))
+        _check(self.lib.zv_euler_sample(self.h, _ptr(x), _ptr(text_c), _ptr(speech_c), _ptr(pm),
+                                        B, T, int(num_step), float(guidance_scale),
+                                        float(t_start), float(t_end), float(t_shift), _stream()))
+        return x
+
+    def text_encode(self, tokens: torch.Tensor, padding_mask: torch.Tensor,
+                    spk: Optional[torch.Tensor] = None) -> torch.Tensor:
+        B, S = tokens.shape
+        tokens = tokens.to(self.device, torch.int64).contiguous()
+        pm = self._mask(padding_mask, (B, S))
+        if spk is not None:
+            spk = spk.to(self.device, torch.int8).contiguous()
+        out = torch.empty((B, S, self.cfg.feat_dim), dtype=torch.float32, device=self.device)
+        _check(self.lib.zv_text_encode(self.h, _ptr(tokens), _ptr(pm), _ptr(spk), B, S, _ptr(out),
+                                       _stream()))
+        return out
+
+    def text_condition(self, embed, tokens_lens, features_lens, num_frames: int):
+        B, S, C = embed.shape
+        embed = self._f32(embed, "embed")
+        tl = tokens_lens.to(self.device, torch.int32).contiguous()
+        fl = features_lens.to(self.device, torch.int32).contiguous()
+        out = torch.empty((B, num_frames, C), dtype=torch.float32, device=self.device)
+        _check(self.lib.zv_text_condition(self.h, _ptr(embed), B, S, _ptr(tl), _ptr(fl),
+                                          int(num_frames), _ptr(out), _stream()))
+        return out
+
+    def speech_condition(self, prompt_features, prompt_lens, num_frames: int):
+        B, Tp, F = prompt_features.shape
+        pf = self._f32(prompt_features, "prompt_features")
+        pl = prompt_lens.to(self.device, torch.int32).contiguous()
+        out = torch.empty((B, num_frames, F), dtype=torch.float32, device=self.device)
+        _check(self.lib.zv_speech_condition(self.h, _ptr(pf), B, Tp, F, _ptr(pl), int(num_frames),
+                                            _ptr(out), _stream()))
+        return out
