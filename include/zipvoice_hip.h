@@ -81,6 +81,17 @@ int zv_reserve(zv_handle h, int max_batch, int max_frames);
 /* Total bytes of device memory held (weights + workspace). */
 int64_t zv_device_bytes(zv_handle h);
 
+/* Launch profiler (process-wide): when enabled, every GEMM / attention launch is
+ * bracketed by HIP events on its stream.  zv_profile(0/1) also clears the log;
+ * zv_profile_report writes a JSON object {kernel: {launches, flops, bytes, ms}}
+ * (synchronises on the recorded events). */
+int zv_profile(int enable);
+int zv_profile_report(char* buf, int buflen);
+
+/* GEMM microbenchmark (random bf16 operands): average ms per launch of tile
+ * variant `variant` for C(M,N) = A(M,K) W(N,K)^T, fp32 (out_bf16=0) or bf16 output. */
+int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_bf16, float* ms_out);
+
 /* Raw decoder: v = fm_decoder(cat[xt, text_c, speech_c], t, pad, g).
  *  t:      [N] timesteps;  guidance: [N] (distill only, else NULL)
  *  xt, speech_c: [N, T, Fx]; text_c: [N, T, feat_dim]; pad: [N, T] uint8 (1 = padded) or NULL

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -81,3 +82,41 @@ __device__ __forceinline__ void store4(bf16* p, const float (&v)[4]) {
 
 __host__ __device__ static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 __host__ __device__ static inline long round_up(long a, long b) { return (a + b - 1) / b * b; }
+
+// ---------------------------------------------------------------------------
+// optional per-launch profiler (HIP events on the launch stream), used by
+// bench.py to measure the dominant kernel's average duration live.
+// ---------------------------------------------------------------------------
+#include <vector>
+struct ZvProfRec {
+  const char* name;
+  double flops;
+  double bytes;
+  hipEvent_t e0, e1;
+};
+struct ZvProfiler {
+  bool on = false;
+  std::vector<ZvProfRec> recs;
+};
+extern ZvProfiler g_zv_prof;
+
+struct ZvProfScope {
+  ZvProfRec rec;
+  hipStream_t s;
+  bool active;
+  ZvProfScope(const char* name, double flops, double bytes, hipStream_t st)
+      : s(st), active(g_zv_prof.on) {
+    if (active) {
+      rec.name = name; rec.flops = flops; rec.bytes = bytes;
+      (void)hipEventCreate(&rec.e0);
+      (void)hipEventCreate(&rec.e1);
+      (void)hipEventRecord(rec.e0, s);
+    }
+  }
+  ~ZvProfScope() {
+    if (active) {
+      (void)hipEventRecord(rec.e1, s);
+      g_zv_prof.recs.push_back(rec);
+    }
+  }
+};

@@ -21,6 +21,7 @@
 #include "../../include/zipvoice_hip.h"
 
 static thread_local std::string g_last_error;
+ZvProfiler g_zv_prof;
 
 namespace {
 
@@ -84,15 +85,37 @@ struct DBuf {
   ~DBuf() { if (p) (void)hipFree(p); }
 };
 
+struct Act {           // GEMM operand in HBM: bf16 hi (+ lo in fp32-accurate mode)
+  bf16* h = nullptr;
+  bf16* l = nullptr;
+  long ld = 0;
+};
+
+struct ActBuf {
+  DBuf h, l;
+  Act get(long rows, long ld, bool split) {
+    Act a;
+    a.ld = ld;
+    a.h = h.get<bf16>((size_t)rows * ld);
+    a.l = split ? l.get<bf16>((size_t)rows * ld) : nullptr;
+    return a;
+  }
+  size_t bytes() const { return h.bytes + l.bytes; }
+};
+
 struct Workspace {
-  DBuf xin, main, dsrc, cur, qkp, W, hidden, dwout, sa_v, sa_o, na_o;
-  DBuf temb0, temb1, tstack, tvec, gvec, posP, mask2, maskds, vout, emb;
+  // fp32 residual streams
+  DBuf main, dsrc, cur, temb0, temb1, tstack, tvec, gvec, posP, mask2, maskds, vout;
+  // bf16 (hi/lo) GEMM operands
+  ActBuf xin, main_a, dsrc_a, cur_a, qkp, W, hidden, na_y, na_xt, na_o, sa_vt, sa_o, glu, dw, emb;
   size_t bytes() const {
     size_t s = 0;
-    for (const DBuf* b : {&xin, &main, &dsrc, &cur, &qkp, &W, &hidden, &dwout, &sa_v, &sa_o, &na_o,
-                          &temb0, &temb1, &tstack, &tvec, &gvec, &posP, &mask2, &maskds, &vout,
-                          &emb})
+    for (const DBuf* b : {&main, &dsrc, &cur, &temb0, &temb1, &tstack, &tvec, &gvec, &posP, &mask2,
+                          &maskds, &vout})
       s += b->bytes;
+    for (const ActBuf* b : {&xin, &main_a, &dsrc_a, &cur_a, &qkp, &W, &hidden, &na_y, &na_xt, &na_o,
+                            &sa_vt, &sa_o, &glu, &dw, &emb})
+      s += b->bytes();
     return s;
   }
 };
@@ -148,7 +171,9 @@ struct zv_engine {
     ZV_CHECK(hipMemcpy(d, v.data(), numel * sizeof(float), hipMemcpyHostToDevice));
     return d;
   }
-  Linear make_linear(const std::string& prefix, int N, int K, bool bias, bool keep_f32) {
+  // perm (optional): row n of the device matrix is row perm[n] of the reference weight
+  Linear make_linear(const std::string& prefix, int N, int K, bool bias, bool keep_f32,
+                     const std::vector<int>* perm = nullptr) {
     Linear L;
     L.N = N; L.K = K;
     L.Npad = (int)round_up(N, W_NPAD);
@@ -157,7 +182,8 @@ struct zv_engine {
     std::vector<bf16> hi((size_t)L.Npad * L.Kpad, (bf16)0.f), lo(hi.size(), (bf16)0.f);
     for (int n = 0; n < N; ++n)
       for (int k = 0; k < K; ++k) {
-        float v = w[(size_t)n * K + k];
+        const int src = perm ? (*perm)[n] : n;
+        float v = w[(size_t)src * K + k];
         bf16 h = (bf16)v;
         hi[(size_t)n * L.Kpad + k] = h;
         lo[(size_t)n * L.Kpad + k] = (bf16)(v - (float)h);
@@ -170,8 +196,39 @@ struct zv_engine {
       L.w32 = dalloc<float>((size_t)N * K);
       ZV_CHECK(hipMemcpy(L.w32, w.data(), (size_t)N * K * sizeof(float), hipMemcpyHostToDevice));
     }
-    if (bias) L.b = upload_f32(prefix + ".bias", N);
+    if (bias) {
+      if (perm) {
+        const auto& b = take(prefix + ".bias", N);
+        std::vector<float> pb(N);
+        for (int n = 0; n < N; ++n) pb[n] = b[(*perm)[n]];
+        L.b = dalloc<float>(N);
+        ZV_CHECK(hipMemcpy(L.b, pb.data(), N * sizeof(float), hipMemcpyHostToDevice));
+      } else {
+        L.b = upload_f32(prefix + ".bias", N);
+      }
+    }
     return L;
+  }
+  // NonlinAttention in_proj rows [s | x | y] -> groups of 48 = [s16 | x16 | y16]
+  static std::vector<int> perm_na(int hid) {
+    std::vector<int> p(3 * hid);
+    for (int g = 0; g < hid / 16; ++g)
+      for (int i = 0; i < 16; ++i) {
+        p[g * 48 + i] = g * 16 + i;
+        p[g * 48 + 16 + i] = hid + g * 16 + i;
+        p[g * 48 + 32 + i] = 2 * hid + g * 16 + i;
+      }
+    return p;
+  }
+  // ConvolutionModule in_proj rows [x | s] -> groups of 32 = [x16 | s16]
+  static std::vector<int> perm_glu(int C) {
+    std::vector<int> p(2 * C);
+    for (int g = 0; g < C / 16; ++g)
+      for (int i = 0; i < 16; ++i) {
+        p[g * 32 + i] = g * 16 + i;
+        p[g * 32 + 16 + i] = C + g * 16 + i;
+      }
+    return p;
   }
   Linear make_small(const std::string& prefix, int N, int K, bool bias) {
     Linear L;
@@ -189,6 +246,7 @@ struct zv_engine {
     Z.qd = cfg.query_head_dim; Z.pd = cfg.pos_head_dim; Z.vd = cfg.value_head_dim;
     Z.pos_dim = cfg.pos_dim; Z.temb_dim = temb_dim;
     ZV_REQUIRE(Z.qd == ATT_QD && Z.pd == ATT_PD, "engine supports query_head_dim=32, pos_head_dim=4");
+    ZV_REQUIRE(heads * Z.vd <= 64, "num_heads * value_head_dim must be <= 64");
     for (size_t i = 0; i < in_dims.size(); ++i) {
       std::string s = two_stream ? "." + std::to_string(i) : "";
       Z.in_proj.push_back(make_linear(pre + "in_proj" + s, dim, in_dims[i], true, false));
@@ -232,12 +290,14 @@ struct zv_engine {
           W.ff_out[f] = make_linear(fp + "out_proj", dim, hs[f], true, false);
         }
         const int hid = 3 * dim / 4;
-        W.na_in = make_linear(lp + "nonlin_attention.in_proj", 3 * hid, dim, true, false);
+        ZV_REQUIRE(hid % 16 == 0 && dim % 64 == 0, "encoder dim must be a multiple of 64");
+        const std::vector<int> pna = perm_na(hid), pglu = perm_glu(dim);
+        W.na_in = make_linear(lp + "nonlin_attention.in_proj", 3 * hid, dim, true, false, &pna);
         W.na_out = make_linear(lp + "nonlin_attention.out_proj", dim, hid, true, false);
         W.ks = ks[s];
         for (int c = 0; c < 2; ++c) {
           std::string cp = lp + "conv_module" + std::to_string(c + 1) + ".";
-          W.conv_in[c] = make_linear(cp + "in_proj", 2 * dim, dim, true, false);
+          W.conv_in[c] = make_linear(cp + "in_proj", 2 * dim, dim, true, false, &pglu);
           W.conv_out[c] = make_linear(cp + "out_proj", dim, dim, true, false);
           W.dw_w[c] = upload_f32(cp + "depthwise_conv.weight", (size_t)dim * W.ks);
           W.dw_b[c] = upload_f32(cp + "depthwise_conv.bias", dim);
@@ -354,157 +414,165 @@ struct zv_engine {
     ZV_LAUNCH_CHECK();
   }
 
-  struct Epi {
-    int act = 0;
-    const void* mul = nullptr; long ldmul = 0;
+  struct Out {              // epilogue of a linear
+    float* C = nullptr; long ldc = 0;
+    Act act;               // bf16 hi/lo copy (act.h null = none)
+    int act_fn = 0;
     const float* resid = nullptr;
     const float* rowvec = nullptr; long rowvec_ld = 0; int rows_per_group = 1;
     const float* orig = nullptr; const float* byp = nullptr;
   };
 
-  template <typename TAct, int SPLIT, typename TA, typename TC>
-  void linear(const Linear& L, const TA* A, long lda, long M, TC* C, long ldc, const Epi& e,
-              hipStream_t s) {
+  static GemmParams gp_linear(const Linear& Lw, const Act& A, long M) {
     GemmParams p{};
-    p.M = (int)M; p.N = L.N; p.K = L.K; p.nz2 = 1;
-    p.A = A; p.lda = lda;
-    p.B = L.hi; p.B_lo = L.lo; p.ldb = L.Kpad;
-    p.C = C; p.ldc = ldc;
-    p.bias = L.b; p.act = e.act;
-    p.mul = e.mul; p.ldmul = e.ldmul;
-    p.resid = e.resid; p.rowvec = e.rowvec; p.rowvec_ld = e.rowvec_ld;
-    p.rows_per_group = e.rows_per_group; p.orig = e.orig; p.byp = e.byp;
-    launch_gemm<128, 128, 32, 2, 2, TA, BMODE_NK, bf16, SPLIT, TC, TAct>(p, 1, s);
+    p.M = (int)M; p.N = Lw.N; p.K = Lw.K; p.nz2 = 1; p.Brows = Lw.Npad;
+    p.Ah = A.h; p.Al = A.l; p.lda = A.ld;
+    p.Bh = Lw.hi; p.Bl = Lw.lo; p.ldb = Lw.Kpad;
+    p.bias = Lw.b; p.rows_per_group = 1; p.rpb = 1;
+    return p;
+  }
+
+  template <int SPLIT>
+  void linear(const Linear& Lw, const Act& A, long M, const Out& o, hipStream_t s) {
+    GemmParams p = gp_linear(Lw, A, M);
+    p.act = o.act_fn;
+    p.C = o.C; p.ldc = o.ldc;
+    p.Ch = o.act.h; p.Cl = o.act.l; p.ldch = o.act.ld;
+    p.resid = o.resid; p.rowvec = o.rowvec; p.rowvec_ld = o.rowvec_ld;
+    p.rows_per_group = o.rows_per_group; p.orig = o.orig; p.byp = o.byp;
+    if (Lw.N <= 64)
+      launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD>(p, 1, s, SPLIT == 3 ? "gemm_fp32" : "gemm_bf16");
+    else
+      launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD>(p, 1, s, SPLIT == 3 ? "gemm_fp32" : "gemm_bf16");
   }
 
   // ---------------------------------------------------------------- one layer
   // Zipformer2EncoderLayer.forward at inference (zipformer.py:489-642).
-  // src: layer input (kept as src_orig, overwritten with the output);
-  // cur: holds src + temb on entry (working residual stream).
-  template <typename TAct, int SPLIT>
-  void layer(const ZipformerW& Z, const LayerW& W, Workspace& ws, float* src, float* cur, int B,
-             int L, const uint8_t* pad, const float* pe, const float* temb, bool has_next,
-             hipStream_t s) {
-    using TW = TAct;
+  // src/src_a: layer input (kept as src_orig, overwritten with the output);
+  // cur/cur_a: src + temb on entry (working residual stream).
+  template <int SPLIT>
+  void layer(const ZipformerW& Z, const LayerW& W, Workspace& ws, float* src, Act src_a,
+             float* cur, Act cur_a, int B, int L, const uint8_t* pad, const float* pe,
+             const float* temb, bool has_next, hipStream_t s) {
+    const bool split = SPLIT == 3;
     const long M = (long)B * L;
     const int D = Z.dim, H = Z.heads;
-    const long ldw = round_up(L, 64);
-    Epi none;
+    const long Lpad = round_up(L, 64);
+    const char* tag_att = split ? "gemm_attn_fp32" : "gemm_attn_bf16";
     // positional projection (2L-1, H*pd)
     float* posP = ws.posP.get<float>((size_t)(2 * L - 1) * H * Z.pd);
     {
       Linear pl; pl.N = H * Z.pd; pl.K = Z.pos_dim; pl.w32 = W.pos_w;
       small_linear(pl, pe, Z.pos_dim, 2 * L - 1, posP, H * Z.pd, 0, nullptr, s);
     }
-    // attention weights from the layer input
+    // attention weights from the layer input (zipformer.py:526)
     const int qkpN = W.attn_in.N;
-    TAct* qkp = ws.qkp.get<TAct>(M * qkpN);
-    linear<TAct, SPLIT>(W.attn_in, src, D, M, qkp, qkpN, none, s);
-    TW* Wt = ws.W.get<TW>((size_t)H * M * ldw);
+    Act qkp = ws.qkp.get(M, qkpN, split);
+    { Out o; o.act = qkp; linear<SPLIT>(W.attn_in, src_a, M, o, s); }
+    Act Wt = ws.W.get((long)H * M, Lpad, split);
     {
-      AttnParams ap{qkp, qkpN, posP, pad, Wt, ldw, B, L, H};
-      launch_attn_softmax<TAct, SPLIT, TW>(ap, s);
+      AttnParams ap{qkp.h, qkp.l, qkpN, posP, pad, Wt.h, Wt.l, Lpad, B, L, H};
+      launch_attn_softmax<SPLIT>(ap, s);
     }
-    TAct* hidden = ws.hidden.get<TAct>(M * std::max({W.ff_in[2].N, W.na_in.N, W.conv_in[0].N}));
-    auto ff = [&](int f, const Epi& outepi) {
-      Epi e1; e1.act = 1;
-      linear<TAct, SPLIT>(W.ff_in[f], cur, D, M, hidden, W.ff_in[f].N, e1, s);
-      linear<TAct, SPLIT>(W.ff_out[f], hidden, W.ff_in[f].N, M, cur, D, outepi, s);
+    Out res;                       // cur = cur + module(cur), with the hi/lo copy
+    res.C = cur; res.ldc = D; res.resid = cur; res.act = cur_a;
+    auto ff = [&](int f, const Out& oe) {
+      Act hid = ws.hidden.get(M, W.ff_in[f].N, split);
+      Out o1; o1.act = hid; o1.act_fn = 1;          // SwooshL fused (scaling.py:1322-1334)
+      linear<SPLIT>(W.ff_in[f], cur_a, M, o1, s);
+      linear<SPLIT>(W.ff_out[f], hid, M, oe, s);
     };
-    Epi res; res.resid = cur;
-    // FF1
-    ff(0, res);
-    // NonlinAttention (head 0 of the weights)
-    {
+    ff(0, res);                                       // FF1 (:536)
+    {                                                 // NonlinAttention (:542-562)
       const int hid = W.na_in.N / 3;
-      linear<TAct, SPLIT>(W.na_in, cur, D, M, hidden, 3 * hid, none, s);
-      hipLaunchKernelGGL((zv_na_gate_kernel<TAct>), grid1d(M * hid), dim3(256), 0, s, hidden, M,
-                         hid, (long)3 * hid);
-      ZV_LAUNCH_CHECK();
-      TAct* nao = ws.na_o.get<TAct>(M * hid);
-      GemmParams p{};
-      p.M = L; p.N = hid; p.K = L; p.nz2 = B;
-      p.A = Wt; p.lda = ldw; p.sA2 = (long)L * ldw;
-      p.B = hidden + hid; p.ldb = 3 * hid; p.sB2 = (long)L * 3 * hid;
-      p.C = nao; p.ldc = hid; p.sC2 = (long)L * hid;
-      p.mul = hidden + 2 * hid; p.ldmul = 3 * hid; p.smul2 = (long)L * 3 * hid;
-      p.rows_per_group = 1;
-      launch_gemm<128, 128, 32, 2, 2, TW, BMODE_KN, TAct, SPLIT, TAct, TAct>(p, B, s);
-      linear<TAct, SPLIT>(W.na_out, nao, hid, M, cur, D, res, s);
+      Act y = ws.na_y.get(M, hid, split);
+      Act xt = ws.na_xt.get((long)B * hid, Lpad, split);
+      GemmParams p = gp_linear(W.na_in, cur_a, M);
+      p.Ch = y.h; p.Cl = y.l; p.ldch = y.ld;
+      p.Cth = xt.h; p.Ctl = xt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)hid * Lpad;
+      launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na");
+      Act nao = ws.na_o.get(M, round_up(hid, 64), split);
+      GemmParams q{};
+      q.M = L; q.N = hid; q.K = L; q.nz2 = B; q.Brows = hid;
+      q.Ah = Wt.h; q.Al = Wt.l; q.lda = Lpad; q.sA2 = (long)L * Lpad;     // head 0
+      q.Bh = xt.h; q.Bl = xt.l; q.ldb = Lpad; q.sB2 = (long)hid * Lpad;
+      q.Ch = nao.h; q.Cl = nao.l; q.ldch = nao.ld; q.sCh2 = (long)L * nao.ld;
+      q.mulh = y.h; q.mull = y.l; q.ldmul = y.ld; q.smul2 = (long)L * y.ld;
+      q.rows_per_group = 1; q.rpb = 1;
+      launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD>(q, B, s, tag_att);
+      linear<SPLIT>(W.na_out, nao, M, res, s);
     }
-    auto self_attn = [&](int a) {
+    auto self_attn = [&](int a) {                     // SelfAttention (:564-570, :600-606)
       const int vd = Z.vd, HV = H * vd;
-      TAct* v = ws.sa_v.get<TAct>(M * HV);
-      TAct* o = ws.sa_o.get<TAct>(M * HV);
-      linear<TAct, SPLIT>(W.sa_in[a], cur, D, M, v, HV, none, s);
-      GemmParams p{};
-      p.M = L; p.N = vd; p.K = L; p.nz2 = B;
-      p.A = Wt; p.lda = ldw; p.sA1 = M * ldw; p.sA2 = (long)L * ldw;
-      p.B = v; p.ldb = HV; p.sB1 = vd; p.sB2 = (long)L * HV;
-      p.C = o; p.ldc = HV; p.sC1 = vd; p.sC2 = (long)L * HV;
-      p.rows_per_group = 1;
-      launch_gemm<64, 16, 32, 4, 1, TW, BMODE_KN, TAct, SPLIT, TAct, TAct>(p, H * B, s);
-      Epi e = res;
+      Act vt = ws.sa_vt.get((long)B * HV, Lpad, split);
+      Act o = ws.sa_o.get(M, 64, split);
+      GemmParams p = gp_linear(W.sa_in[a], cur_a, M);
+      p.Cth = vt.h; p.Ctl = vt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)HV * Lpad;
+      launch_gemm<128, 64, 2, 2, SPLIT, EPI_TRANS>(p, 1, s, split ? "gemm_fp32_t" : "gemm_bf16_t");
+      GemmParams q{};
+      q.M = L; q.N = vd; q.K = L; q.nz2 = B; q.Brows = vd;
+      q.Ah = Wt.h; q.Al = Wt.l; q.lda = Lpad; q.sA1 = M * Lpad; q.sA2 = (long)L * Lpad;
+      q.Bh = vt.h; q.Bl = vt.l; q.ldb = Lpad; q.sB1 = (long)vd * Lpad; q.sB2 = (long)HV * Lpad;
+      q.Ch = o.h; q.Cl = o.l; q.ldch = o.ld; q.sCh1 = vd; q.sCh2 = (long)L * o.ld;
+      q.rows_per_group = 1; q.rpb = 1;
+      launch_gemm<128, 16, 4, 1, SPLIT, EPI_STD>(q, H * B, s, tag_att);
+      Out e = res;
       if (temb) { e.rowvec = temb; e.rowvec_ld = D; e.rows_per_group = L; }
-      linear<TAct, SPLIT>(W.sa_out[a], o, HV, M, cur, D, e, s);
+      linear<SPLIT>(W.sa_out[a], o, M, e, s);
     };
-    auto conv = [&](int c) {
-      linear<TAct, SPLIT>(W.conv_in[c], cur, D, M, hidden, 2 * D, none, s);
-      hipLaunchKernelGGL((zv_glu_mask_kernel<TAct>), grid1d(M * D), dim3(256), 0, s, hidden, M, D,
-                         (long)2 * D, pad, L);
-      ZV_LAUNCH_CHECK();
-      TAct* dw = ws.dwout.get<TAct>(M * D);
-      hipLaunchKernelGGL((zv_dwconv_swooshr_kernel<TAct>), grid1d(M * D), dim3(256), 0, s, hidden,
-                         (long)2 * D, W.dw_w[c], W.dw_b[c], dw, (long)D, B, L, D, W.ks);
-      ZV_LAUNCH_CHECK();
-      linear<TAct, SPLIT>(W.conv_out[c], dw, D, M, cur, D, res, s);
+    auto conv = [&](int c) {                          // ConvolutionModule (:1638-1680)
+      Act g = ws.glu.get(M, D, split);
+      GemmParams p = gp_linear(W.conv_in[c], cur_a, M);
+      p.Ch = g.h; p.Cl = g.l; p.ldch = g.ld; p.rowmask = pad;
+      launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu");
+      Act dw = ws.dw.get(M, D, split);
+      launch_dwconv(g.h, g.l, g.ld, W.dw_w[c], W.dw_b[c], dw.h, dw.l, dw.ld, B, L, D, W.ks, s);
+      linear<SPLIT>(W.conv_out[c], dw, M, res, s);
     };
-    self_attn(0);                 // SA1 (+ temb)
-    conv(0);                      // conv1
-    {                             // FF2 + bypass_mid
-      Epi e = res; e.orig = src; e.byp = W.bypass_mid;
+    self_attn(0);                                     // SA1 (+ temb)
+    conv(0);                                          // conv1
+    {                                                 // FF2 + bypass_mid (:593-598)
+      Out e = res; e.orig = src; e.byp = W.bypass_mid;
       ff(1, e);
     }
-    self_attn(1);                 // SA2 (+ temb)
-    conv(1);                      // conv2
-    ff(2, res);                   // FF3
+    self_attn(1);                                     // SA2 (+ temb)
+    conv(1);                                          // conv2
+    ff(2, res);                                       // FF3
     // BiasNorm + bypass -> src; next layer's working copy (src + temb) -> cur
     hipLaunchKernelGGL(zv_biasnorm_bypass_kernel, dim3(cdiv(M, 4)), dim3(256), 0, s, cur, src,
-                       W.norm_bias, W.norm_log_scale, W.bypass, src, has_next ? cur : nullptr,
-                       temb, L, M, D);
+                       W.norm_bias, W.norm_log_scale, W.bypass, src, src_a.h, src_a.l,
+                       has_next ? cur : nullptr, cur_a.h, cur_a.l, (long)D, temb, L, M, D);
     ZV_LAUNCH_CHECK();
   }
 
   // ---------------------------------------------------------------- one stack
-  template <typename TAct, int SPLIT>
-  void stack(const ZipformerW& Z, const StackW& S, Workspace& ws, float* src, int B, int L,
-             const uint8_t* pad, const float* temb, hipStream_t s) {
+  template <int SPLIT>
+  void stack(const ZipformerW& Z, const StackW& S, Workspace& ws, float* src, Act src_a, int B,
+             int L, const uint8_t* pad, const float* temb, hipStream_t s) {
     const long M = (long)B * L;
+    const bool split = SPLIT == 3;
     float* cur = ws.cur.get<float>(M * Z.dim);
-    if (temb) {
-      hipLaunchKernelGGL(zv_add_rowvec_kernel, grid1d(M * Z.dim), dim3(256), 0, s, src, temb, cur,
-                         M, Z.dim, L);
-    } else {
-      ZV_CHECK(hipMemcpyAsync(cur, src, M * Z.dim * sizeof(float), hipMemcpyDeviceToDevice, s));
-    }
+    Act cur_a = ws.cur_a.get(M, Z.dim, split);
+    hipLaunchKernelGGL(zv_stack_entry_kernel, grid1d(M * Z.dim), dim3(256), 0, s, src, temb, cur,
+                       src_a.h, src_a.l, cur_a.h, cur_a.l, (long)Z.dim, M, Z.dim, L);
     ZV_LAUNCH_CHECK();
     const float* pe = pe_table(L, s);
     for (size_t li = 0; li < S.layers.size(); ++li)
-      layer<TAct, SPLIT>(Z, S.layers[li], ws, src, cur, B, L, pad, pe, temb,
-                         li + 1 < S.layers.size(), s);
+      layer<SPLIT>(Z, S.layers[li], ws, src, src_a, cur, cur_a, B, L, pad, pe, temb,
+                   li + 1 < S.layers.size(), s);
   }
 
   // ---------------------------------------------------------------- TTSZipformer
-  // TTSZipformer.forward (zipformer.py:242-293).  xin (N, T, Fin); t/g (N) device.
-  template <typename TAct, int SPLIT>
-  void zipformer(const ZipformerW& Z, Workspace& ws, const float* xin, int Fin, int sidx, int N,
-                 int T, const uint8_t* pad, const float* t, const float* g, float* out,
-                 hipStream_t s) {
+  // TTSZipformer.forward (zipformer.py:242-293).  xin: bf16 hi/lo (N*T, Fin); t/g (N).
+  template <int SPLIT>
+  void zipformer(const ZipformerW& Z, Workspace& ws, Act xin, int sidx, int N, int T,
+                 const uint8_t* pad, const float* t, const float* g, float* out, hipStream_t s) {
     const long M = (long)N * T;
     const int D = Z.dim;
+    const bool split = SPLIT == 3;
     float* main = ws.main.get<float>(M * D);
-    Epi none;
-    linear<TAct, SPLIT>(Z.in_proj[sidx], xin, Fin, M, main, D, none, s);
+    Act main_a = ws.main_a.get(M, D, split);
+    { Out o; o.C = main; o.ldc = D; linear<SPLIT>(Z.in_proj[sidx], xin, M, o, s); }
     // time embedding MLP (zipformer.py:267-278) + per-stack projections (:726-729)
     float* tstack = nullptr;
     if (Z.has_time) {
@@ -518,8 +586,7 @@ struct zv_engine {
         hipLaunchKernelGGL(zv_timestep_embed_kernel, grid1d(N * E), dim3(256), 0, s, g,
                            temb_freqs, e1, N, E);
         ZV_LAUNCH_CHECK();
-        // e0 = e0 + guidance_scale_embed(e1)
-        small_linear(Z.guid, e1, E, N, e0, E, 0, e0, s);
+        small_linear(Z.guid, e1, E, N, e0, E, 0, e0, s);   // e0 += guidance_scale_embed(e1)
       }
       small_linear(Z.te0, e0, E, N, e1, 2 * E, 0, nullptr, s);
       small_linear(Z.te2, e1, 2 * E, N, e0, E, 1, nullptr, s);
@@ -532,10 +599,11 @@ struct zv_engine {
       const StackW& S = Z.stacks[si];
       const float* te = tstack ? tstack + si * (size_t)N * D : nullptr;
       if (S.ds == 1) {
-        stack<TAct, SPLIT>(Z, S, ws, main, N, T, pad, te, s);
+        stack<SPLIT>(Z, S, ws, main, main_a, N, T, pad, te, s);
       } else {
         const int dL = (T + S.ds - 1) / S.ds;
         float* d = ws.dsrc.get<float>((size_t)N * dL * D);
+        Act d_a = ws.dsrc_a.get((long)N * dL, D, split);
         hipLaunchKernelGGL(zv_downsample_kernel, grid1d((long)N * dL * D), dim3(256), 0, s, main, d,
                            N, T, dL, D, S.ds, S.ds_w);
         ZV_LAUNCH_CHECK();
@@ -546,38 +614,44 @@ struct zv_engine {
                              N, T, dL, S.ds);
           ZV_LAUNCH_CHECK();
         }
-        stack<TAct, SPLIT>(Z, S, ws, d, N, dL, pds, te, s);
+        stack<SPLIT>(Z, S, ws, d, d_a, N, dL, pds, te, s);
         hipLaunchKernelGGL(zv_upsample_combine_kernel, grid1d(M * D), dim3(256), 0, s, main, d,
                            S.combiner, main, N, T, dL, D, S.ds);
         ZV_LAUNCH_CHECK();
       }
     }
-    linear<TAct, SPLIT>(Z.out_proj[sidx], main, D, M, out, Z.out_proj[sidx].N, none, s);
+    // factors end with 1: the last stack's final BiasNorm wrote main_a
+    ZV_REQUIRE(Z.stacks.back().ds == 1, "last stack must have downsampling factor 1");
+    { Out o; o.C = out; o.ldc = Z.out_proj[sidx].N; linear<SPLIT>(Z.out_proj[sidx], main_a, M, o, s); }
   }
 
-  template <typename TAct, int SPLIT>
-  void decoder_dispatch(const float* xin, int Fin, int N, int T, const uint8_t* pad,
-                        const float* t, const float* g, float* out, hipStream_t s) {
+  Act build_xin(Workspace& ws, const float* x, const float* tc, const float* sc, int B, int T,
+                int Fx, int copies, int zero_speech, hipStream_t s) {
+    const int Ft = cfg.feat_dim, Fin = 2 * Fx + Ft;
+    const bool split = cfg.precision == ZV_FP32;
+    const long N = (long)copies * B;
+    Act xin = ws.xin.get(N * T, round_up(Fin, 64), split);
+    hipLaunchKernelGGL(zv_build_input_kernel, grid1d(N * T * Fin), dim3(256), 0, s, x, tc, sc,
+                       xin.h, xin.l, xin.ld, B, T, Fx, Ft, Fx, copies, zero_speech);
+    ZV_LAUNCH_CHECK();
+    return xin;
+  }
+
+  void decoder(Act xin, int Fin, int N, int T, const uint8_t* pad, const float* t, const float* g,
+               float* out, hipStream_t s) {
     int sidx = 0;
     if (stereo()) sidx = (Fin == dec.in_proj[0].K) ? 0 : 1;
     ZV_REQUIRE(Fin == dec.in_proj[sidx].K, "decoder input width does not match in_proj");
-    zipformer<TAct, SPLIT>(dec, ws_dec, xin, Fin, sidx, N, T, pad, t, g, out, s);
+    if (cfg.precision == ZV_FP32) zipformer<3>(dec, ws_dec, xin, sidx, N, T, pad, t, g, out, s);
+    else zipformer<1>(dec, ws_dec, xin, sidx, N, T, pad, t, g, out, s);
   }
-  void decoder(const float* xin, int Fin, int N, int T, const uint8_t* pad, const float* t,
-               const float* g, float* out, hipStream_t s) {
-    if (cfg.precision == ZV_FP32) decoder_dispatch<float, 3>(xin, Fin, N, T, pad, t, g, out, s);
-    else decoder_dispatch<bf16, 1>(xin, Fin, N, T, pad, t, g, out, s);
-  }
-
-  int out_width(int Fx) const { return Fx; }
 
   // guided velocity at scalar t for B un-doubled rows (solver.py:40-165)
   void velocity(float t, float gscale, const float* x, const float* tc, const float* sc,
                 const uint8_t* pad, int B, int T, float* vout, bool euler, float dt,
                 hipStream_t s) {
     const int Fx = stereo() ? 2 * cfg.feat_dim : cfg.feat_dim;
-    const int Ft = cfg.feat_dim;
-    const int Fin = 2 * Fx + Ft;
+    const int Fin = 2 * Fx + cfg.feat_dim;
     const bool cfg_on = !distill() && gscale != 0.0f;
     const int copies = cfg_on ? 2 : 1;
     const int N = copies * B;
@@ -587,10 +661,7 @@ struct zv_engine {
       if (t > 0.5f) zero_speech = 1;
       else g = gscale * 2.0f;
     }
-    float* xin = ws_dec.xin.get<float>((size_t)N * T * Fin);
-    hipLaunchKernelGGL(zv_build_input_kernel, grid1d((long)N * T * Fin), dim3(256), 0, s, x, tc,
-                       sc, xin, B, T, Fx, Ft, Fx, copies, zero_speech);
-    ZV_LAUNCH_CHECK();
+    Act xin = build_xin(ws_dec, x, tc, sc, B, T, Fx, copies, zero_speech, s);
     const uint8_t* padN = pad;
     if (pad && copies == 2) {
       uint8_t* p2 = ws_dec.mask2.get<uint8_t>((size_t)N * T);
@@ -639,13 +710,13 @@ struct zv_engine {
                    float* out, hipStream_t s) {
     const long n = (long)B * S;
     const int E = cfg.text_embed_dim;
-    float* emb = ws_txt.emb.get<float>(n * E);
-    hipLaunchKernelGGL(zv_embed_kernel, grid1d(n * E), dim3(256), 0, s, tok, embed_table, emb, n, E);
+    const bool split = cfg.precision == ZV_FP32;
+    Act emb = ws_txt.emb.get(n, round_up(E, 64), split);
+    hipLaunchKernelGGL(zv_embed_kernel, grid1d(n * E), dim3(256), 0, s, tok, embed_table, emb.h,
+                       emb.l, emb.ld, n, E);
     ZV_LAUNCH_CHECK();
-    if (cfg.precision == ZV_FP32)
-      zipformer<float, 3>(txt, ws_txt, emb, E, 0, B, S, pad, nullptr, nullptr, out, s);
-    else
-      zipformer<bf16, 1>(txt, ws_txt, emb, E, 0, B, S, pad, nullptr, nullptr, out, s);
+    if (split) zipformer<3>(txt, ws_txt, emb, 0, B, S, pad, nullptr, nullptr, out, s);
+    else zipformer<1>(txt, ws_txt, emb, 0, B, S, pad, nullptr, nullptr, out, s);
     if (spk && spk_table) {
       hipLaunchKernelGGL(zv_spk_add_kernel, grid1d(n * cfg.feat_dim), dim3(256), 0, s, out, spk,
                          spk_table, n, cfg.feat_dim);
@@ -673,6 +744,30 @@ struct zv_engine {
 static void check_ready(zv_handle h) {
   ZV_REQUIRE(h != nullptr, "null engine handle");
   ZV_REQUIRE(h->ready, "engine weights not finalized (call zv_finalize)");
+}
+
+// GEMM microbenchmark on random operands: C(M,N) fp32 = A(M,K) . W(N,K)^T
+static __global__ void zv_fill_rand_bf16(bf16* p, long n, unsigned seed) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    unsigned x = (unsigned)i * 2654435761u ^ seed;
+    x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+    p[i] = (bf16)(((float)(x & 0xffff) / 65535.0f) * 2.0f - 1.0f);
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN, int STAGES>
+static float bench_variant(GemmParams p, int iters, hipStream_t s) {
+  hipEvent_t e0, e1;
+  ZV_CHECK(hipEventCreate(&e0)); ZV_CHECK(hipEventCreate(&e1));
+  launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES>(p, 1, s, "bench");
+  ZV_CHECK(hipEventRecord(e0, s));
+  for (int i = 0; i < iters; ++i) launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES>(p, 1, s, "bench");
+  ZV_CHECK(hipEventRecord(e1, s));
+  ZV_CHECK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  ZV_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  ZV_CHECK(hipEventDestroy(e0)); ZV_CHECK(hipEventDestroy(e1));
+  return ms / iters;
 }
 
 extern "C" {
@@ -718,6 +813,77 @@ int zv_reserve(zv_handle h, int max_batch, int max_frames) {
   ZV_API_END
 }
 
+int zv_profile(int enable) {
+  ZV_API_BEGIN
+  for (auto& r : g_zv_prof.recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
+  g_zv_prof.recs.clear();
+  g_zv_prof.on = enable != 0;
+  ZV_API_END
+}
+
+int zv_profile_report(char* buf, int buflen) {
+  ZV_API_BEGIN
+  ZV_REQUIRE(buf && buflen > 0, "bad buffer");
+  struct Agg { int n = 0; double flops = 0, bytes = 0, ms = 0; };
+  std::map<std::string, Agg> agg;
+  for (auto& r : g_zv_prof.recs) {
+    ZV_CHECK(hipEventSynchronize(r.e1));
+    float ms = 0.f;
+    ZV_CHECK(hipEventElapsedTime(&ms, r.e0, r.e1));
+    Agg& a = agg[r.name];
+    a.n += 1; a.flops += r.flops; a.bytes += r.bytes; a.ms += ms;
+  }
+  std::string js = "{";
+  bool first = true;
+  for (auto& kv : agg) {
+    char tmp[512];
+    snprintf(tmp, sizeof(tmp), "%s\"%s\": {\"launches\": %d, \"flops\": %.6e, \"bytes\": %.6e, \"ms\": %.6f}",
+             first ? "" : ", ", kv.first.c_str(), kv.second.n, kv.second.flops, kv.second.bytes,
+             kv.second.ms);
+    js += tmp;
+    first = false;
+  }
+  js += "}";
+  ZV_REQUIRE((int)js.size() < buflen, "report buffer too small");
+  memcpy(buf, js.c_str(), js.size() + 1);
+  ZV_API_END
+}
+
+int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_bf16, float* ms_out) {
+  ZV_API_BEGIN
+  hipStream_t s = nullptr;
+  const long Kp = round_up(K, 64), Np = round_up(N, 256);
+  bf16 *A, *W, *Ch = nullptr;
+  float* C = nullptr;
+  ZV_CHECK(hipMalloc(&A, (size_t)M * Kp * 2));
+  ZV_CHECK(hipMalloc(&W, (size_t)Np * Kp * 2));
+  if (out_bf16) ZV_CHECK(hipMalloc(&Ch, (size_t)M * N * 2));
+  else ZV_CHECK(hipMalloc(&C, (size_t)M * N * 4));
+  hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(4096), dim3(256), 0, s, A, (long)M * Kp, 1u);
+  hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(4096), dim3(256), 0, s, W, (long)Np * Kp, 2u);
+  GemmParams p{};
+  p.M = M; p.N = N; p.K = K; p.nz2 = 1; p.Brows = (int)Np;
+  p.Ah = A; p.lda = Kp; p.Bh = W; p.ldb = Kp;
+  p.C = C; p.ldc = N; p.Ch = Ch; p.ldch = N; p.rows_per_group = 1; p.rpb = 1;
+  float ms = -1.f;
+  switch (variant) {
+    case 0: ms = bench_variant<128, 128, 2, 2, 2>(p, iters, s); break;
+    case 1: ms = bench_variant<128, 128, 2, 2, 3>(p, iters, s); break;
+    case 2: ms = bench_variant<256, 128, 4, 2, 2>(p, iters, s); break;
+    case 3: ms = bench_variant<256, 128, 4, 2, 3>(p, iters, s); break;
+    case 4: ms = bench_variant<128, 64, 2, 2, 3>(p, iters, s); break;
+    case 5: ms = bench_variant<128, 256, 2, 4, 2>(p, iters, s); break;
+    case 6: ms = bench_variant<128, 128, 2, 2, 4>(p, iters, s); break;
+    case 7: ms = bench_variant<256, 128, 2, 2, 2>(p, iters, s); break;
+    default: throw std::invalid_argument("unknown variant");
+  }
+  *ms_out = ms;
+  ZV_CHECK(hipFree(A)); ZV_CHECK(hipFree(W));
+  if (C) ZV_CHECK(hipFree(C));
+  if (Ch) ZV_CHECK(hipFree(Ch));
+  ZV_API_END
+}
+
 int64_t zv_device_bytes(zv_handle h) {
   if (!h) return 0;
   return (int64_t)(h->weight_bytes + h->ws_dec.bytes() + h->ws_txt.bytes());
@@ -731,12 +897,8 @@ int zv_fm_decoder(zv_handle h, const float* t, const float* guidance, const floa
   ZV_REQUIRE(N > 0 && T > 0, "empty batch");
   ZV_REQUIRE(!h->distill() || guidance, "distill model needs a guidance_scale");
   hipStream_t s = (hipStream_t)stream;
-  const int Ft = h->cfg.feat_dim;
-  const int Fin = 2 * Fx + Ft;
-  float* xin = h->ws_dec.xin.get<float>((size_t)N * T * Fin);
-  hipLaunchKernelGGL(zv_build_input_kernel, grid1d((long)N * T * Fin), dim3(256), 0, s, xt,
-                     text_c, speech_c, xin, N, T, Fx, Ft, Fx, 1, 0);
-  ZV_LAUNCH_CHECK();
+  const int Fin = 2 * Fx + h->cfg.feat_dim;
+  Act xin = h->build_xin(h->ws_dec, xt, text_c, speech_c, N, T, Fx, 1, 0, s);
   h->decoder(xin, Fin, N, T, pad, t, h->distill() ? guidance : nullptr, v_out, s);
   ZV_API_END
 }

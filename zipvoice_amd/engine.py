@@ -59,6 +59,9 @@ SIGNATURES = {
     "zv_finalize": (_I, [_P]),
     "zv_reserve": (_I, [_P, _I, _I]),
     "zv_device_bytes": (ctypes.c_int64, [_P]),
+    "zv_profile": (_I, [_I]),
+    "zv_bench_gemm": (_I, [_I, _I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_float)]),
+    "zv_profile_report": (_I, [ctypes.c_char_p, _I]),
     "zv_fm_decoder": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
     "zv_velocity": (_I, [_P, _F, _F, _P, _P, _P, _P, _I, _I, _P, _P]),
     "zv_euler_sample": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _F, _P]),
@@ -117,6 +120,20 @@ def make_zv_config(cfg: ModelConfig, precision: str) -> ZvConfig:
               "pos_head_dim", "pos_dim", "vocab_size", "pad_id", "spk_a_id", "spk_b_id"):
         setattr(c, f, int(getattr(cfg, f)))
     return c
+
+
+def profile(enable: bool):
+    """Enable/disable (and clear) the engine's per-launch event profiler."""
+    lib = load_library()
+    _check(lib.zv_profile(1 if enable else 0))
+
+
+def profile_report() -> dict:
+    import json
+    lib = load_library()
+    buf = ctypes.create_string_buffer(1 << 16)
+    _check(lib.zv_profile_report(buf, len(buf)))
+    return json.loads(buf.value.decode())
 
 
 def _ptr(t: Optional[torch.Tensor]):
