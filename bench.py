@@ -72,10 +72,10 @@ def run_step(model, inp, world, rank):
         features_lens=inp["features_lens"], t_shift=T_SHIFT, duration="real",
         num_step=NUM_STEP, guidance_scale=GUIDANCE, x0=inp["x0"])
     if world > 1:
-        import torch.distributed as dist
-        out = torch.empty((world,) + tuple(gen.shape), dtype=gen.dtype, device=gen.device)
-        dist.all_gather_into_tensor(out, gen.contiguous())
-        gen = out
+        # the one exchange of the data-parallel path: reassemble the generated mel
+        # batch on every rank (RCCL all-gather over xGMI), zipvoice_amd/dist.py
+        from zipvoice_amd.dist import all_gather_padded
+        gen, gen_lens = all_gather_padded(gen, gen_lens)
     return gen
 
 

@@ -1,0 +1,78 @@
+"""Multi-process data-parallel path on CPU (gloo, world_size 2): sharding is
+balanced and covers every item once; the final all-gather reassembles ragged
+per-rank outputs in the original order."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from zipvoice_amd.dist import all_gather_padded, shard_bounds
+
+
+def test_shard_bounds_cover_and_balance():
+    for costs in ([1] * 32, [5, 1, 1, 1, 1, 1, 1, 5], list(range(1, 20)), [3], [], [2, 2]):
+        for world in (1, 2, 4, 8):
+            b = shard_bounds(costs, world)
+            assert len(b) == world
+            assert b[0][0] == 0 and b[-1][1] == len(costs)
+            for (lo, hi), (lo2, _) in zip(b, b[1:]):
+                assert hi == lo2 and lo <= hi
+    b = shard_bounds([1] * 32, 8)
+    assert all(hi - lo == 4 for lo, hi in b)
+    # ragged costs: no rank above the ideal share + one max item
+    costs = [int(c) for c in torch.randint(100, 3000, (64,), generator=torch.Generator().manual_seed(0))]
+    for world in (2, 4, 8):
+        b = shard_bounds(costs, world)
+        loads = [sum(costs[lo:hi]) for lo, hi in b]
+        assert max(loads) <= sum(costs) / world + max(costs)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        costs = [10 + 7 * i % 13 for i in range(7)]
+        lo, hi = shard_bounds(costs, world)[rank]
+        # each "utterance" i produces costs[i] frames of value i (3 features)
+        T = max([costs[i] for i in range(lo, hi)], default=1)
+        x = torch.zeros((hi - lo, T, 3))
+        for j, i in enumerate(range(lo, hi)):
+            x[j, :costs[i]] = float(i)
+        lens = torch.tensor([costs[i] for i in range(lo, hi)], dtype=torch.int64)
+        allx, alll = all_gather_padded(x, lens)
+        q.put((rank, allx.numpy().tolist(), alll.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_all_gather_reassembles_batch_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    costs = [10 + 7 * i % 13 for i in range(7)]
+    for rank, allx, alll in res:
+        assert alll == costs
+        allx = torch.tensor(allx)
+        assert allx.shape[0] == 7
+        for i in range(7):
+            assert torch.all(allx[i, :costs[i]] == float(i))
+            assert torch.all(allx[i, costs[i]:] == 0)

@@ -1,0 +1,69 @@
+"""Data-parallel batch sharding across the GPUs of one node.
+
+The reference runs inference on a single device, one sentence at a time
+(``infer_zipvoice.py:568-577``, ``:431-452``); utterances are independent, so the
+MI355X build shards a batch across one process per GPU with no data-path
+collective, and uses exactly one exchange at the end: an all-gather (RCCL over
+xGMI on GPUs, gloo in the CPU tests) of the per-utterance output lengths and the
+padded outputs, which reassembles the batch in its original order on every rank.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(costs: Sequence[float], world: int) -> List[Tuple[int, int]]:
+    """Split items 0..n-1 into `world` contiguous ranges of roughly equal total
+    cost (e.g. frames per utterance).  Every rank gets a range (possibly empty)."""
+    n = len(costs)
+    total = float(sum(costs))
+    bounds = []
+    start, acc = 0, 0.0
+    for r in range(world - 1):
+        target = total * (r + 1) / world
+        end = start
+        while end < n and acc + costs[end] <= target + 1e-9:
+            acc += costs[end]
+            end += 1
+        # take one more item when that lands closer to the ideal boundary
+        if end < n and abs(acc + costs[end] - target) < abs(acc - target):
+            acc += costs[end]
+            end += 1
+        bounds.append((start, end))
+        start = end
+    bounds.append((start, n))
+    return bounds
+
+
+def local_slice(items: Sequence, costs: Sequence[float], rank: int, world: int):
+    lo, hi = shard_bounds(costs, world)[rank]
+    return lo, hi, list(items[lo:hi])
+
+
+def all_gather_padded(x: torch.Tensor, lens: torch.Tensor, group=None):
+    """All-gather a (b_r, T_r, F) tensor with per-row lengths (b_r,) from every
+    rank, where b_r and T_r may differ per rank.  Returns the concatenated
+    (sum b_r, max T, F) tensor (rows in rank order, zero padded) and lengths."""
+    world = dist.get_world_size(group)
+    dev = x.device
+    shape = torch.tensor([x.shape[0], x.shape[1]], dtype=torch.int64, device=dev)
+    shapes = [torch.zeros_like(shape) for _ in range(world)]
+    dist.all_gather(shapes, shape, group=group)
+    shapes = [tuple(int(v) for v in s.tolist()) for s in shapes]
+    bmax = max(s[0] for s in shapes)
+    tmax = max(s[1] for s in shapes)
+    F = x.shape[2]
+    pad = torch.zeros((bmax, tmax, F), dtype=x.dtype, device=dev)
+    pad[:x.shape[0], :x.shape[1]] = x
+    lpad = torch.zeros((bmax,), dtype=torch.int64, device=dev)
+    lpad[:lens.shape[0]] = lens.to(torch.int64)
+    outs = [torch.empty_like(pad) for _ in range(world)]
+    louts = [torch.empty_like(lpad) for _ in range(world)]
+    dist.all_gather(outs, pad, group=group)
+    dist.all_gather(louts, lpad, group=group)
+    rows = [o[:s[0]] for o, s in zip(outs, shapes)]
+    lrows = [l[:s[0]] for l, s in zip(louts, shapes)]
+    return torch.cat(rows, 0), torch.cat(lrows, 0)
