@@ -138,3 +138,24 @@ def test_long_sequence_properties():
     v3 = m.forward_fm_decoder(torch.tensor(0.4), torch.cat([x, x.flip(1)]),
                               torch.cat([tc, tc]), torch.cat([sc, sc]), None)
     assert (v3[:1] - v1).abs().max().item() < 1e-5
+
+
+def test_materialized_attention_path_matches(monkeypatch):
+    """A/B: the W-materialising attention path (ZV_ATTN_MATERIALIZE=1) and the fused
+    flash-style consumers give the same decoder output (fp32 mode)."""
+    from zipvoice_amd.config import default_config
+    from zipvoice_amd.models import build_model
+    from zipvoice_amd.weights import synthetic_state_dict
+    d = load("decoder_fwd.npz")
+    cfg = default_config("zipvoice")
+    monkeypatch.setenv("ZV_ATTN_MATERIALIZE", "1")
+    m = build_model(cfg, precision="fp32")
+    m.load_state_dict(synthetic_state_dict(cfg, 0))
+    m = m.to("cuda:0")
+    args = dict(t=torch.tensor(float(d["t"])), xt=cuda(d["x"]),
+                text_condition=cuda(d["text_condition"]),
+                speech_condition=cuda(d["speech_condition"]), padding_mask=cuda(d["padding_mask"]))
+    v_mat = m.forward_fm_decoder(**args)
+    check(v_mat, d["v"], "fp32", "decoder_fwd (materialised W)")
+    v_fused = model("zipvoice", "fp32").forward_fm_decoder(**args)
+    assert (v_mat - v_fused).abs().max().item() < 1e-4

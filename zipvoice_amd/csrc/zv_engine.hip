@@ -7,6 +7,7 @@
 // or bf16 hi/lo pairs (ZV_FP32).  Weights are stored [Npad][Kpad] bf16 hi
 // (+ lo) zero-padded to the GEMM tile grid, biases fp32.
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <map>
@@ -18,6 +19,7 @@
 #include "zv_gemm.inc"
 #include "zv_attn.inc"
 #include "zv_elem.inc"
+#include "zv_flash.inc"
 #include "../../include/zipvoice_hip.h"
 
 static thread_local std::string g_last_error;
@@ -105,13 +107,13 @@ struct ActBuf {
 
 struct Workspace {
   // fp32 residual streams
-  DBuf main, dsrc, cur, temb0, temb1, tstack, tvec, gvec, posP, mask2, maskds, vout;
+  DBuf main, dsrc, cur, temb0, temb1, tstack, tvec, gvec, posP, mask2, maskds, vout, stats;
   // bf16 (hi/lo) GEMM operands
   ActBuf xin, main_a, dsrc_a, cur_a, qkp, W, hidden, na_y, na_xt, na_o, sa_vt, sa_o, glu, dw, emb;
   size_t bytes() const {
     size_t s = 0;
     for (const DBuf* b : {&main, &dsrc, &cur, &temb0, &temb1, &tstack, &tvec, &gvec, &posP, &mask2,
-                          &maskds, &vout})
+                          &maskds, &vout, &stats})
       s += b->bytes;
     for (const ActBuf* b : {&xin, &main_a, &dsrc_a, &cur_a, &qkp, &W, &hidden, &na_y, &na_xt, &na_o,
                             &sa_vt, &sa_o, &glu, &dw, &emb})
@@ -143,7 +145,12 @@ struct zv_engine {
   std::map<int, float*> pe_cache; // L -> (2L-1, pos_dim)
   Workspace ws_dec, ws_txt;
 
-  explicit zv_engine(const zv_config& c) : cfg(c) {}
+  bool materialize_attn = false;   // A/B: ZV_ATTN_MATERIALIZE=1 keeps the W-materialising path
+
+  explicit zv_engine(const zv_config& c) : cfg(c) {
+    const char* e = getenv("ZV_ATTN_MATERIALIZE");
+    materialize_attn = e && e[0] == '1';
+  }
   ~zv_engine() {
     for (void* p : allocs) (void)hipFree(p);
     for (auto& kv : pe_cache) (void)hipFree(kv.second);
@@ -469,10 +476,19 @@ struct zv_engine {
     const int qkpN = W.attn_in.N;
     Act qkp = ws.qkp.get(M, qkpN, split);
     { Out o; o.act = qkp; linear<SPLIT>(W.attn_in, src_a, M, o, s); }
-    Act Wt = ws.W.get((long)H * M, Lpad, split);
-    {
+    // attention: either materialise W (reference structure, A/B path) or keep
+    // only per-row softmax statistics and recompute scores inside each consumer
+    Act Wt;
+    FlashParams fp{};
+    if (materialize_attn) {
+      Wt = ws.W.get((long)H * M, Lpad, split);
       AttnParams ap{qkp.h, qkp.l, qkpN, posP, pad, Wt.h, Wt.l, Lpad, B, L, H};
       launch_attn_softmax<SPLIT>(ap, s);
+    } else {
+      fp.qh = qkp.h; fp.ql = qkp.l; fp.ldq = qkpN; fp.P = posP; fp.key_pad = pad;
+      fp.stats = ws.stats.get<float2>((size_t)H * M);
+      fp.B = B; fp.L = L; fp.H = H;
+      launch_attn_stats<SPLIT>(fp, s);
     }
     Out res;                       // cur = cur + module(cur), with the hi/lo copy
     res.C = cur; res.ldc = D; res.resid = cur; res.act = cur_a;
@@ -492,14 +508,24 @@ struct zv_engine {
       p.Cth = xt.h; p.Ctl = xt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)hid * Lpad;
       launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na");
       Act nao = ws.na_o.get(M, round_up(hid, 64), split);
-      GemmParams q{};
-      q.M = L; q.N = hid; q.K = L; q.nz2 = B; q.Brows = hid;
-      q.Ah = Wt.h; q.Al = Wt.l; q.lda = Lpad; q.sA2 = (long)L * Lpad;     // head 0
-      q.Bh = xt.h; q.Bl = xt.l; q.ldb = Lpad; q.sB2 = (long)hid * Lpad;
-      q.Ch = nao.h; q.Cl = nao.l; q.ldch = nao.ld; q.sCh2 = (long)L * nao.ld;
-      q.mulh = y.h; q.mull = y.l; q.ldmul = y.ld; q.smul2 = (long)L * y.ld;
-      q.rows_per_group = 1; q.rpb = 1;
-      launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD>(q, B, s, tag_att);
+      if (materialize_attn) {
+        GemmParams q{};
+        q.M = L; q.N = hid; q.K = L; q.nz2 = B; q.Brows = hid;
+        q.Ah = Wt.h; q.Al = Wt.l; q.lda = Lpad; q.sA2 = (long)L * Lpad;     // head 0
+        q.Bh = xt.h; q.Bl = xt.l; q.ldb = Lpad; q.sB2 = (long)hid * Lpad;
+        q.Ch = nao.h; q.Cl = nao.l; q.ldch = nao.ld; q.sCh2 = (long)L * nao.ld;
+        q.mulh = y.h; q.mull = y.l; q.ldmul = y.ld; q.smul2 = (long)L * y.ld;
+        q.rows_per_group = 1; q.rpb = 1;
+        launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD>(q, B, s, tag_att);
+      } else {
+        FlashParams f = fp;
+        f.vh = xt.h; f.vl = xt.l; f.ldv = Lpad; f.sv_b = (long)hid * Lpad; f.vrows_per_head = 0;
+        f.nv = hid;
+        f.mulh = y.h; f.mull = y.l; f.ldmul = y.ld;
+        f.oh = nao.h; f.ol = nao.l; f.ldo = nao.ld; f.ocol_per_head = 0;
+        if (hid <= 144) launch_attn_apply<SPLIT, 9, 4, true>(f, 1, s);
+        else launch_attn_apply<SPLIT, 24, 4, true>(f, 1, s);
+      }
       linear<SPLIT>(W.na_out, nao, M, res, s);
     }
     auto self_attn = [&](int a) {                     // SelfAttention (:564-570, :600-606)
@@ -509,13 +535,22 @@ struct zv_engine {
       GemmParams p = gp_linear(W.sa_in[a], cur_a, M);
       p.Cth = vt.h; p.Ctl = vt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)HV * Lpad;
       launch_gemm<128, 64, 2, 2, SPLIT, EPI_TRANS>(p, 1, s, split ? "gemm_fp32_t" : "gemm_bf16_t");
-      GemmParams q{};
-      q.M = L; q.N = vd; q.K = L; q.nz2 = B; q.Brows = vd;
-      q.Ah = Wt.h; q.Al = Wt.l; q.lda = Lpad; q.sA1 = M * Lpad; q.sA2 = (long)L * Lpad;
-      q.Bh = vt.h; q.Bl = vt.l; q.ldb = Lpad; q.sB1 = (long)vd * Lpad; q.sB2 = (long)HV * Lpad;
-      q.Ch = o.h; q.Cl = o.l; q.ldch = o.ld; q.sCh1 = vd; q.sCh2 = (long)L * o.ld;
-      q.rows_per_group = 1; q.rpb = 1;
-      launch_gemm<128, 16, 4, 1, SPLIT, EPI_STD>(q, H * B, s, tag_att);
+      if (materialize_attn) {
+        GemmParams q{};
+        q.M = L; q.N = vd; q.K = L; q.nz2 = B; q.Brows = vd;
+        q.Ah = Wt.h; q.Al = Wt.l; q.lda = Lpad; q.sA1 = M * Lpad; q.sA2 = (long)L * Lpad;
+        q.Bh = vt.h; q.Bl = vt.l; q.ldb = Lpad; q.sB1 = (long)vd * Lpad; q.sB2 = (long)HV * Lpad;
+        q.Ch = o.h; q.Cl = o.l; q.ldch = o.ld; q.sCh1 = vd; q.sCh2 = (long)L * o.ld;
+        q.rows_per_group = 1; q.rpb = 1;
+        launch_gemm<128, 16, 4, 1, SPLIT, EPI_STD>(q, H * B, s, tag_att);
+      } else {
+        ZV_REQUIRE(vd <= 16, "value_head_dim > 16 unsupported by the fused kernel");
+        FlashParams f = fp;
+        f.vh = vt.h; f.vl = vt.l; f.ldv = Lpad; f.sv_b = (long)HV * Lpad; f.vrows_per_head = vd;
+        f.nv = vd;
+        f.oh = o.h; f.ol = o.l; f.ldo = o.ld; f.ocol_per_head = vd;
+        launch_attn_apply<SPLIT, 1, 4, false>(f, H, s);
+      }
       Out e = res;
       if (temb) { e.rowvec = temb; e.rowvec_ld = D; e.rows_per_group = L; }
       linear<SPLIT>(W.sa_out[a], o, M, e, s);
