@@ -82,15 +82,18 @@ int zv_reserve(zv_handle h, int max_batch, int max_frames);
 int64_t zv_device_bytes(zv_handle h);
 
 /* Launch profiler (process-wide): when enabled, every GEMM / attention launch is
- * bracketed by HIP events on its stream.  zv_profile(0/1) also clears the log;
+ * bracketed by HIP events on its stream.  zv_profile(0/1) also clears the log
+ * (2 = on, with GEMM records keyed by shape);
  * zv_profile_report writes a JSON object {kernel: {launches, flops, bytes, ms}}
  * (synchronises on the recorded events). */
 int zv_profile(int enable);
 int zv_profile_report(char* buf, int buflen);
 
 /* GEMM microbenchmark (random bf16 operands): average ms per launch of tile
- * variant `variant` for C(M,N) = A(M,K) W(N,K)^T, fp32 (out_bf16=0) or bf16 output. */
-int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_bf16, float* ms_out);
+ * variant `variant` (+100: one tile per block instead of the persistent grid) for
+ * C(M,N) = A(M,K) W(N,K)^T with out_mode 0 = fp32 C, 1 = bf16 C, 2 = residual
+ * (C += ..., fp32, plus a bf16 copy), 3 = SwooshL -> bf16. */
+int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, float* ms_out);
 
 /* Raw decoder: v = fm_decoder(cat[xt, text_c, speech_c], t, pad, g).
  *  t:      [N] timesteps;  guidance: [N] (distill only, else NULL)

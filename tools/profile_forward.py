@@ -19,6 +19,7 @@ ap.add_argument("--precision", default="bf16")
 ap.add_argument("--iters", type=int, default=2)
 ap.add_argument("--B", type=int, default=32)
 ap.add_argument("--T", type=int, default=1219)
+ap.add_argument("--report", action="store_true", help="per-shape event-profiler table")
 a = ap.parse_args()
 cfg = default_config("zipvoice")
 m = build_model(cfg, precision=a.precision)
@@ -34,3 +35,17 @@ for _ in range(a.iters):
     v = m.engine.velocity(0.3, 1.0, x, tc, sc, pm)
 torch.cuda.synchronize()
 print("ok", float(v.abs().mean()))
+if a.report:
+    from zipvoice_amd import engine
+    engine.profile(True, detail=True)
+    m.engine.velocity(0.3, 1.0, x, tc, sc, pm)
+    torch.cuda.synchronize()
+    rep = engine.profile_report()
+    engine.profile(False)
+    tot = sum(r["ms"] for r in rep.values())
+    print(f"# one guided forward, event-profiled launches: {tot:.3f} ms")
+    print(f"{'launch':64s} {'n':>4s} {'ms':>8s} {'avg_us':>8s} {'TF/s':>7s} {'pct':>5s}")
+    for k, r in sorted(rep.items(), key=lambda kv: -kv[1]["ms"]):
+        tf = r["flops"] / (r["ms"] * 1e-3) / 1e12 if r["flops"] else 0.0
+        print(f"{k:64s} {r['launches']:4d} {r['ms']:8.3f} {1e3 * r['ms'] / r['launches']:8.1f} "
+              f"{tf:7.1f} {100 * r['ms'] / tot:5.1f}")

@@ -32,16 +32,18 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // ---------------------------------------------------------------------------
 
 // SwooshLForward, scaling.py:1174-1180: log(1+exp(x-4)) (x-4 if inf) - 0.08x - 0.035
+// (v_exp_f32 / v_log_f32 forms of the same formula: the GEMM epilogue runs it
+// on every hidden activation)
 __device__ __forceinline__ float swoosh_l(float x) {
   float xo = x - 4.0f;
-  float ls = logf(1.0f + expf(xo));
+  float ls = __logf(1.0f + __expf(xo));
   if (isinf(ls)) ls = xo;
   return ls - 0.08f * x - 0.035f;
 }
 // SwooshRForward, scaling.py:1185-1191
 __device__ __forceinline__ float swoosh_r(float x) {
   float xo = x - 1.0f;
-  float ls = logf(1.0f + expf(xo));
+  float ls = __logf(1.0f + __expf(xo));
   if (isinf(ls)) ls = xo;
   return ls - 0.08f * x - 0.313261687f;
 }
@@ -88,14 +90,16 @@ __host__ __device__ static inline long round_up(long a, long b) { return (a + b 
 // bench.py to measure the dominant kernel's average duration live.
 // ---------------------------------------------------------------------------
 #include <vector>
+#include <string>
 struct ZvProfRec {
-  const char* name;
+  std::string name;
   double flops;
   double bytes;
   hipEvent_t e0, e1;
 };
 struct ZvProfiler {
   bool on = false;
+  bool detail = false;     // key GEMM records by shape (zv_profile(2))
   std::vector<ZvProfRec> recs;
 };
 extern ZvProfiler g_zv_prof;

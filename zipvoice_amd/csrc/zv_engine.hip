@@ -486,7 +486,7 @@ struct zv_engine {
       launch_attn_softmax<SPLIT>(ap, s);
     } else {
       fp.qh = qkp.h; fp.ql = qkp.l; fp.ldq = qkpN; fp.P = posP; fp.key_pad = pad;
-      fp.stats = ws.stats.get<float2>((size_t)H * M);
+      fp.stats = ws.stats.get<float2>((size_t)M);     // head 0 only (NonlinAttention)
       fp.B = B; fp.L = L; fp.H = H;
       launch_attn_stats<SPLIT>(fp, s);
     }
@@ -523,8 +523,10 @@ struct zv_engine {
         f.nv = hid;
         f.mulh = y.h; f.mull = y.l; f.ldmul = y.ld;
         f.oh = nao.h; f.ol = nao.l; f.ldo = nao.ld; f.ocol_per_head = 0;
-        if (hid <= 144) launch_attn_apply<SPLIT, 9, 4, true>(f, 1, s);
-        else launch_attn_apply<SPLIT, 24, 4, true>(f, 1, s);
+        constexpr int QTILES = SPLIT == 3 ? 4 : 8;
+        if (hid <= 128) launch_attn_na<SPLIT, 1, QTILES>(f, s);
+        else if (hid <= 256) launch_attn_na<SPLIT, 2, QTILES>(f, s);
+        else launch_attn_na<SPLIT, 3, QTILES>(f, s);
       }
       linear<SPLIT>(W.na_out, nao, M, res, s);
     }
@@ -544,12 +546,11 @@ struct zv_engine {
         q.rows_per_group = 1; q.rpb = 1;
         launch_gemm<128, 16, 4, 1, SPLIT, EPI_STD>(q, H * B, s, tag_att);
       } else {
-        ZV_REQUIRE(vd <= 16, "value_head_dim > 16 unsupported by the fused kernel");
         FlashParams f = fp;
         f.vh = vt.h; f.vl = vt.l; f.ldv = Lpad; f.sv_b = (long)HV * Lpad; f.vrows_per_head = vd;
         f.nv = vd;
         f.oh = o.h; f.ol = o.l; f.ldo = o.ld; f.ocol_per_head = vd;
-        launch_attn_apply<SPLIT, 1, 4, false>(f, H, s);
+        launch_attn_sa<SPLIT>(f, s);
       }
       Out e = res;
       if (temb) { e.rowvec = temb; e.rowvec_ld = D; e.rows_per_group = L; }
@@ -791,12 +792,13 @@ static __global__ void zv_fill_rand_bf16(bf16* p, long n, unsigned seed) {
 }
 
 template <int BM, int BN, int WGM, int WGN, int STAGES>
-static float bench_variant(GemmParams p, int iters, hipStream_t s) {
+static float bench_variant(GemmParams p, int iters, bool persistent, hipStream_t s) {
   hipEvent_t e0, e1;
   ZV_CHECK(hipEventCreate(&e0)); ZV_CHECK(hipEventCreate(&e1));
-  launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES>(p, 1, s, "bench");
+  launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES>(p, 1, s, "bench", persistent);
   ZV_CHECK(hipEventRecord(e0, s));
-  for (int i = 0; i < iters; ++i) launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES>(p, 1, s, "bench");
+  for (int i = 0; i < iters; ++i)
+    launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES>(p, 1, s, "bench", persistent);
   ZV_CHECK(hipEventRecord(e1, s));
   ZV_CHECK(hipEventSynchronize(e1));
   float ms = 0.f;
@@ -853,6 +855,7 @@ int zv_profile(int enable) {
   for (auto& r : g_zv_prof.recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
   g_zv_prof.recs.clear();
   g_zv_prof.on = enable != 0;
+  g_zv_prof.detail = enable == 2;
   ZV_API_END
 }
 
@@ -884,32 +887,39 @@ int zv_profile_report(char* buf, int buflen) {
   ZV_API_END
 }
 
-int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_bf16, float* ms_out) {
+int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, float* ms_out) {
   ZV_API_BEGIN
   hipStream_t s = nullptr;
   const long Kp = round_up(K, 64), Np = round_up(N, 256);
   bf16 *A, *W, *Ch = nullptr;
   float* C = nullptr;
+  const bool persistent = variant < 100;
+  variant %= 100;
   ZV_CHECK(hipMalloc(&A, (size_t)M * Kp * 2));
   ZV_CHECK(hipMalloc(&W, (size_t)Np * Kp * 2));
-  if (out_bf16) ZV_CHECK(hipMalloc(&Ch, (size_t)M * N * 2));
-  else ZV_CHECK(hipMalloc(&C, (size_t)M * N * 4));
+  if (out_mode != 0) ZV_CHECK(hipMalloc(&Ch, (size_t)M * N * 2));
+  if (out_mode == 0 || out_mode == 2) {
+    ZV_CHECK(hipMalloc(&C, (size_t)M * N * 4));
+    ZV_CHECK(hipMemsetAsync(C, 0, (size_t)M * N * 4, s));
+  }
   hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(4096), dim3(256), 0, s, A, (long)M * Kp, 1u);
   hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(4096), dim3(256), 0, s, W, (long)Np * Kp, 2u);
   GemmParams p{};
   p.M = M; p.N = N; p.K = K; p.nz2 = 1; p.Brows = (int)Np;
   p.Ah = A; p.lda = Kp; p.Bh = W; p.ldb = Kp;
   p.C = C; p.ldc = N; p.Ch = Ch; p.ldch = N; p.rows_per_group = 1; p.rpb = 1;
+  if (out_mode == 2) p.resid = C;
+  if (out_mode == 3) p.act = 1;
   float ms = -1.f;
   switch (variant) {
-    case 0: ms = bench_variant<128, 128, 2, 2, 2>(p, iters, s); break;
-    case 1: ms = bench_variant<128, 128, 2, 2, 3>(p, iters, s); break;
-    case 2: ms = bench_variant<256, 128, 4, 2, 2>(p, iters, s); break;
-    case 3: ms = bench_variant<256, 128, 4, 2, 3>(p, iters, s); break;
-    case 4: ms = bench_variant<128, 64, 2, 2, 3>(p, iters, s); break;
-    case 5: ms = bench_variant<128, 256, 2, 4, 2>(p, iters, s); break;
-    case 6: ms = bench_variant<128, 128, 2, 2, 4>(p, iters, s); break;
-    case 7: ms = bench_variant<256, 128, 2, 2, 2>(p, iters, s); break;
+    case 0: ms = bench_variant<128, 128, 2, 2, 2>(p, iters, persistent, s); break;
+    case 1: ms = bench_variant<128, 128, 2, 2, 3>(p, iters, persistent, s); break;
+    case 2: ms = bench_variant<256, 128, 4, 2, 2>(p, iters, persistent, s); break;
+    case 3: ms = bench_variant<256, 128, 4, 2, 3>(p, iters, persistent, s); break;
+    case 4: ms = bench_variant<128, 64, 2, 2, 3>(p, iters, persistent, s); break;
+    case 5: ms = bench_variant<128, 256, 2, 4, 2>(p, iters, persistent, s); break;
+    case 6: ms = bench_variant<128, 128, 2, 2, 4>(p, iters, persistent, s); break;
+    case 7: ms = bench_variant<256, 128, 2, 2, 2>(p, iters, persistent, s); break;
     default: throw std::invalid_argument("unknown variant");
   }
   *ms_out = ms;

@@ -122,16 +122,17 @@ def make_zv_config(cfg: ModelConfig, precision: str) -> ZvConfig:
     return c
 
 
-def profile(enable: bool):
-    """Enable/disable (and clear) the engine's per-launch event profiler."""
+def profile(enable: bool, detail: bool = False):
+    """Enable/disable (and clear) the engine's per-launch event profiler;
+    ``detail`` keys the GEMM records by shape."""
     lib = load_library()
-    _check(lib.zv_profile(1 if enable else 0))
+    _check(lib.zv_profile((2 if detail else 1) if enable else 0))
 
 
 def profile_report() -> dict:
     import json
     lib = load_library()
-    buf = ctypes.create_string_buffer(1 << 16)
+    buf = ctypes.create_string_buffer(1 << 20)
     _check(lib.zv_profile_report(buf, len(buf)))
     return json.loads(buf.value.decode())
 
