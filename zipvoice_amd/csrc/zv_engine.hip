@@ -143,6 +143,7 @@ struct zv_engine {
   float* spk_table = nullptr;     // (2, feat_dim)
   float* temb_freqs = nullptr;    // (time_embed_dim/2)
   std::map<int, float*> pe_cache; // L -> (2L-1, pos_dim)
+  std::map<std::pair<const float*, int>, float*> posp_cache;   // (layer pos weight, L) -> (2L-1, H*pd)
   Workspace ws_dec, ws_txt;
 
   bool materialize_attn = false;   // A/B: ZV_ATTN_MATERIALIZE=1 keeps the W-materialising path
@@ -154,6 +155,7 @@ struct zv_engine {
   ~zv_engine() {
     for (void* p : allocs) (void)hipFree(p);
     for (auto& kv : pe_cache) (void)hipFree(kv.second);
+    for (auto& kv : posp_cache) (void)hipFree(kv.second);
   }
 
   // ---------------------------------------------------------------- weights
@@ -415,8 +417,8 @@ struct zv_engine {
   // ---------------------------------------------------------------- launch helpers
   void small_linear(const Linear& L, const float* in, int ldin, int M, float* out, int ldout,
                     int pre, const float* add, hipStream_t s) {
-    int n = M * L.N;
-    hipLaunchKernelGGL(zv_small_linear_kernel, grid1d(n), dim3(256), 0, s, in, ldin, L.w32,
+    const long n = (long)M * L.N;
+    hipLaunchKernelGGL(zv_small_linear_kernel, dim3((unsigned)cdiv(n, 4L)), dim3(256), 0, s, in, ldin, L.w32,
                        L.K, L.b, add, out, ldout, M, L.N, L.K, pre);
     ZV_LAUNCH_CHECK();
   }
@@ -467,8 +469,15 @@ struct zv_engine {
     const long Lpad = round_up(L, 64);
     const char* tag_att = split ? "gemm_attn_fp32" : "gemm_attn_bf16";
     // positional projection (2L-1, H*pd)
-    float* posP = ws.posP.get<float>((size_t)(2 * L - 1) * H * Z.pd);
-    {
+    // depends only on (layer, L): computed once per length and kept (bounded)
+    if (posp_cache.size() > 1024 && !posp_cache.count({W.pos_w, L})) {
+      ZV_CHECK(hipStreamSynchronize(s));
+      for (auto& kv : posp_cache) ZV_CHECK(hipFree(kv.second));
+      posp_cache.clear();
+    }
+    float*& posP = posp_cache[{W.pos_w, L}];
+    if (!posP) {
+      ZV_CHECK(hipMalloc(&posP, (size_t)(2 * L - 1) * H * Z.pd * sizeof(float)));
       Linear pl; pl.N = H * Z.pd; pl.K = Z.pos_dim; pl.w32 = W.pos_w;
       small_linear(pl, pe, Z.pos_dim, 2 * L - 1, posP, H * Z.pd, 0, nullptr, s);
     }
@@ -920,6 +929,9 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
     case 5: ms = bench_variant<128, 256, 2, 4, 2>(p, iters, persistent, s); break;
     case 6: ms = bench_variant<128, 128, 2, 2, 4>(p, iters, persistent, s); break;
     case 7: ms = bench_variant<256, 128, 2, 2, 2>(p, iters, persistent, s); break;
+    case 8: ms = bench_variant<256, 256, 2, 4, 2>(p, iters, persistent, s); break;
+    case 9: ms = bench_variant<256, 128, 2, 4, 2>(p, iters, persistent, s); break;
+    case 10: ms = bench_variant<128, 256, 1, 4, 2>(p, iters, persistent, s); break;
     default: throw std::invalid_argument("unknown variant");
   }
   *ms_out = ms;
