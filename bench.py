@@ -6,9 +6,13 @@ weights — no pretrained weights offline), bf16 MFMA, N_steps=16, batch of 32
 utterances per GPU, each a 3 s prompt (281 frames, 40 prompt tokens) + 10 s of
 generated speech (938 frames, 134 text tokens; duration="real"), so T = 1219
 frames, classifier-free guidance 1.0 (batch doubled to 64 inside the engine),
-t_shift 0.5.  One "step" = one full ``ZipVoice.sample()`` of the batch (text
-encoder, conditions, the 16-step guided Euler loop) plus, for N > 1 GPUs, the
-RCCL all-gather that reassembles the generated mel batch on every rank.
+t_shift 0.5.  One "step" = what the reference's RTF times
+(``infer_zipvoice.py:359-386``): one full ``ZipVoice.sample()`` of the batch
+(text encoder, conditions, the 16-step guided Euler loop) followed by the
+vocoder on the generated features (post-processing + Vocos decode + clamp,
+``:374-378``; synthetic vocos-mel-24khz weights, fp32-accurate mode), plus, for
+N > 1 GPUs, the RCCL all-gather that reassembles the output wav batch on every
+rank.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]
         (N > 1 under torch.distributed.run, one process per GPU).
@@ -65,30 +69,36 @@ def build(precision, device):
     return m.to(device)
 
 
-def run_step(model, inp, world, rank):
+def build_vocoder(device):
+    from zipvoice_amd.vocoder import Vocos
+    return Vocos(precision="fp32").load_synthetic(0).to(device)
+
+
+def run_step(model, vocoder, inp, world, rank):
     gen, gen_lens, _, _ = model.sample(
         tokens=inp["tokens"], prompt_tokens=inp["prompt_tokens"],
         prompt_features=inp["prompt_features"], prompt_features_lens=inp["prompt_features_lens"],
         features_lens=inp["features_lens"], t_shift=T_SHIFT, duration="real",
         num_step=NUM_STEP, guidance_scale=GUIDANCE, x0=inp["x0"])
+    wav = vocoder.decode_features(gen, gen_lens, feat_scale=0.1, feat_bias=0.0, clamp=True)
     if world > 1:
-        # the one exchange of the data-parallel path: reassemble the generated mel
+        # the one exchange of the data-parallel path: reassemble the output wav
         # batch on every rank (RCCL all-gather over xGMI), zipvoice_amd/dist.py
         from zipvoice_amd.dist import all_gather_padded
-        gen, gen_lens = all_gather_padded(gen, gen_lens)
-    return gen
+        wav, _ = all_gather_padded(wav.unsqueeze(-1), gen_lens * HOP)
+    return wav
 
 
-def timed(model, inp, steps, warmup, world, rank):
+def timed(model, vocoder, inp, steps, warmup, world, rank):
     import torch.distributed as dist
     for _ in range(warmup):
-        run_step(model, inp, world, rank)
+        run_step(model, vocoder, inp, world, rank)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
-        run_step(model, inp, world, rank)
+        run_step(model, vocoder, inp, world, rank)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -100,13 +110,13 @@ def timed(model, inp, steps, warmup, world, rank):
     return dt / steps
 
 
-def roofline(model, inp):
+def roofline(model, vocoder, inp):
     """One extra, untimed step with the engine's per-launch HIP-event profiler on:
     the dominant kernel's algorithmic FLOPs per launch / its average duration."""
     from zipvoice_amd import engine
     torch.cuda.synchronize()
     engine.profile(True)
-    run_step(model, inp, 1, 0)
+    run_step(model, vocoder, inp, 1, 0)
     torch.cuda.synchronize()
     rep = engine.profile_report()
     engine.profile(False)
@@ -178,8 +188,9 @@ def main():
         dist.init_process_group("nccl", device_id=device)
 
     model = build(args.precision, device)
+    vocoder = build_vocoder(device)
     inp = make_inputs(rank, device)
-    ms = timed(model, inp, args.steps, args.warmup, world, rank) * 1e3
+    ms = timed(model, vocoder, inp, args.steps, args.warmup, world, rank) * 1e3
     frames = B_PER_GPU * T_GEN * world
     value = frames / (ms * 1e-3)
     audio_s_per_gpu = B_PER_GPU * T_GEN * HOP / SAMPLE_RATE
@@ -197,12 +208,12 @@ def main():
                    "parallelism": f"dp{world}"},
     }
     if rank == 0:
-        result["roofline"] = roofline(model, inp)
+        result["roofline"] = roofline(model, vocoder, inp)
         if world == 1 and not args.no_fp32_mode and args.precision == "bf16":
             del model
             torch.cuda.empty_cache()
             m32 = build("fp32", device)
-            ms32 = timed(m32, inp, 1, 1, 1, 0) * 1e3
+            ms32 = timed(m32, vocoder, inp, 1, 1, 1, 0) * 1e3
             result["fp32_accurate_mode"] = {
                 "ms_per_step": round(ms32, 2),
                 "value": round(B_PER_GPU * T_GEN / (ms32 * 1e-3), 1), "unit": "mel-frames/s",

@@ -27,6 +27,12 @@
  *   zv_speech_condition  speech-condition padding in ZipVoice.sample (zipvoice.py:441-451)
  *   Reference per-step ONNX operator with the same contract as zv_velocity:
  *       fm_decoder.onnx (zipvoice/bin/onnx_export.py:157-204)
+ *   zv_vocoder_*       the vocoder the reference loads and calls after sampling:
+ *                      get_vocoder (zipvoice/bin/infer_zipvoice.py:249-273) ->
+ *                      Vocos.from_hparams + load_state_dict, and
+ *                      `vocoder.decode(pred_features).squeeze(1).clamp(-1, 1)` with the
+ *                      feature post-processing of infer_zipvoice.py:374-378
+ *                      (third-party vocos 0.1.0: Vocos.decode = VocosBackbone + ISTFTHead)
  */
 #ifndef ZIPVOICE_HIP_H
 #define ZIPVOICE_HIP_H
@@ -130,6 +136,45 @@ int zv_text_condition(zv_handle h, const float* embed, int B, int S, const int32
 /* Speech condition: prompt features [B, Tp, F] padded/zeroed to [B, T, F]. */
 int zv_speech_condition(zv_handle h, const float* prompt, int B, int Tp, int F,
                         const int32_t* prompt_lens, int T, float* out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Vocoder (Vocos, mel-24khz configuration: n_mels 100, dim 512, intermediate 1536,
+ * 8 ConvNeXt blocks, ISTFT head n_fft 1024 / hop 256 / padding "same").
+ * ---------------------------------------------------------------------- */
+typedef struct zv_vocoder* zv_vocoder_handle;
+
+/* Mirrors the vocos config.yaml backbone / head init_args. */
+typedef struct {
+  int precision;          /* zv_precision (ZV_FP32 = split-bf16x3 GEMMs, the parity mode) */
+  int n_mels;             /* backbone.input_channels (100) */
+  int dim;                /* backbone.dim (512) */
+  int intermediate_dim;   /* backbone.intermediate_dim (1536) */
+  int num_layers;         /* backbone.num_layers (8) */
+  int n_fft;              /* head.n_fft (1024) */
+  int hop;                /* head.hop_length (256) */
+  int embed_kernel;       /* backbone.embed kernel size (7) */
+  int dw_kernel;          /* ConvNeXt depthwise kernel size (7) */
+} zv_vocoder_config;
+
+zv_vocoder_handle zv_vocoder_create(const zv_vocoder_config* cfg);
+void zv_vocoder_destroy(zv_vocoder_handle v);
+/* Stage one vocos state-dict tensor (e.g. "backbone.convnext.3.pwconv1.weight",
+ * "head.istft.window"); "feature_extractor.*" buffers are accepted and ignored. */
+int zv_vocoder_set_weight(zv_vocoder_handle v, const char* name, const float* host_data,
+                          int64_t numel);
+int zv_vocoder_finalize(zv_vocoder_handle v);
+/* wav[b, :T*hop] = decode(mel_b) for B utterances of up to T frames.
+ *  layout 0: mel [B, n_mels, T] (Vocos.decode input, used as is: pass feat_scale 1, feat_bias 0);
+ *  layout 1: model output [B, T, n_mels], post-processed as x / feat_scale - feat_bias
+ *            (infer_zipvoice.py:374) inside the first kernel.
+ *  lens: [B] int32 device frame counts (NULL = all T): utterance b is decoded on its own
+ *        first lens[b] frames, exactly as a separate call would, and samples from
+ *        lens[b]*hop on are 0.
+ *  clamp: 1 applies clamp(-1, 1) (infer_zipvoice.py:378).  wav: [B, T*hop] fp32. */
+int zv_vocoder_decode(zv_vocoder_handle v, const float* mel, int layout, float feat_scale,
+                      float feat_bias, const int32_t* lens, int B, int T, float* wav, int clamp,
+                      void* stream);
+int64_t zv_vocoder_device_bytes(zv_vocoder_handle v);
 
 #ifdef __cplusplus
 }

@@ -147,10 +147,14 @@ struct zv_engine {
   Workspace ws_dec, ws_txt;
 
   bool materialize_attn = false;   // A/B: ZV_ATTN_MATERIALIZE=1 keeps the W-materialising path
+  int gemm_tile = 0;               // A/B: ZV_GEMM_TILE 0 = 128x128, 1 = 256x128, 2 = 256x256,
+                                   // 3 = 256x128 3-stage (bf16 linears with N >= 256)
 
   explicit zv_engine(const zv_config& c) : cfg(c) {
     const char* e = getenv("ZV_ATTN_MATERIALIZE");
     materialize_attn = e && e[0] == '1';
+    const char* g = getenv("ZV_GEMM_TILE");
+    gemm_tile = g ? atoi(g) : 0;
   }
   ~zv_engine() {
     for (void* p : allocs) (void)hipFree(p);
@@ -449,10 +453,26 @@ struct zv_engine {
     p.Ch = o.act.h; p.Cl = o.act.l; p.ldch = o.act.ld;
     p.resid = o.resid; p.rowvec = o.rowvec; p.rowvec_ld = o.rowvec_ld;
     p.rows_per_group = o.rows_per_group; p.orig = o.orig; p.byp = o.byp;
-    if (Lw.N <= 64)
-      launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD>(p, 1, s, SPLIT == 3 ? "gemm_fp32" : "gemm_bf16");
-    else
-      launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD>(p, 1, s, SPLIT == 3 ? "gemm_fp32" : "gemm_bf16");
+    const char* tag = SPLIT == 3 ? "gemm_fp32" : "gemm_bf16";
+    if (Lw.N <= 64) {
+      launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD>(p, 1, s, tag);
+      return;
+    }
+    if constexpr (SPLIT == 1) {
+      if (gemm_tile == 1 && Lw.N >= 256) {
+        launch_gemm<256, 128, 4, 2, SPLIT, EPI_STD>(p, 1, s, tag);
+        return;
+      }
+      if (gemm_tile == 2 && Lw.N >= 256) {
+        launch_gemm<256, 256, 2, 4, SPLIT, EPI_STD>(p, 1, s, tag);
+        return;
+      }
+      if (gemm_tile == 3 && Lw.N >= 256) {
+        launch_gemm<256, 128, 4, 2, SPLIT, EPI_STD, 3>(p, 1, s, tag);
+        return;
+      }
+    }
+    launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD>(p, 1, s, tag);
   }
 
   // ---------------------------------------------------------------- one layer
@@ -770,6 +790,8 @@ struct zv_engine {
   }
 };
 
+#include "zv_vocoder.inc"
+
 // ===========================================================================
 // C ABI
 // ===========================================================================
@@ -1012,6 +1034,61 @@ int zv_speech_condition(zv_handle h, const float* prompt, int B, int Tp, int F,
                      (hipStream_t)stream, prompt, Tp, prompt_lens, out, B, T, F);
   ZV_LAUNCH_CHECK();
   ZV_API_END
+}
+
+// ---------------------------------------------------------------- vocoder
+zv_vocoder_handle zv_vocoder_create(const zv_vocoder_config* cfg) {
+  try {
+    ZV_REQUIRE(cfg != nullptr, "null vocoder config");
+    ZV_REQUIRE(cfg->precision == ZV_FP32 || cfg->precision == ZV_BF16, "bad precision");
+    ZV_REQUIRE(cfg->n_mels > 0 && cfg->dim > 0 && cfg->intermediate_dim > 0 && cfg->num_layers > 0,
+               "bad vocoder dimensions");
+    ZV_REQUIRE(cfg->embed_kernel % 2 == 1, "embed kernel must be odd");
+    return new zv_vocoder(*cfg);
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return nullptr;
+  }
+}
+
+void zv_vocoder_destroy(zv_vocoder_handle v) { delete v; }
+
+int zv_vocoder_set_weight(zv_vocoder_handle v, const char* name, const float* host_data,
+                          int64_t numel) {
+  ZV_API_BEGIN
+  ZV_REQUIRE(v && name && (host_data || numel == 0), "bad arguments");
+  ZV_REQUIRE(!v->ready, "vocoder already finalized");
+  v->staged[name].assign(host_data, host_data + numel);
+  ZV_API_END
+}
+
+int zv_vocoder_finalize(zv_vocoder_handle v) {
+  ZV_API_BEGIN
+  ZV_REQUIRE(v != nullptr, "null vocoder handle");
+  v->finalize();
+  ZV_API_END
+}
+
+int zv_vocoder_decode(zv_vocoder_handle v, const float* mel, int layout, float feat_scale,
+                      float feat_bias, const int32_t* lens, int B, int T, float* wav, int clamp,
+                      void* stream) {
+  ZV_API_BEGIN
+  ZV_REQUIRE(v != nullptr && v->ready, "vocoder not finalized (call zv_vocoder_finalize)");
+  ZV_REQUIRE(B > 0 && T > 0, "empty batch");
+  ZV_REQUIRE(layout == 0 || layout == 1, "layout must be 0 (B,C,T) or 1 (B,T,C)");
+  ZV_REQUIRE(feat_scale != 0.f, "feat_scale must be nonzero");
+  hipStream_t s = (hipStream_t)stream;
+  if (v->cfg.precision == ZV_FP32)
+    v->decode<3>(mel, layout, feat_scale, feat_bias, lens, B, T, wav, clamp, s);
+  else
+    v->decode<1>(mel, layout, feat_scale, feat_bias, lens, B, T, wav, clamp, s);
+  ZV_API_END
+}
+
+int64_t zv_vocoder_device_bytes(zv_vocoder_handle v) {
+  if (!v) return 0;
+  return (int64_t)(v->weight_bytes + v->x.bytes + v->frames.bytes + v->col.bytes() +
+                   v->h.bytes() + v->hid.bytes() + v->spec.bytes());
 }
 
 }  // extern "C"

@@ -68,6 +68,13 @@ SIGNATURES = {
     "zv_text_encode": (_I, [_P, _P, _P, _P, _I, _I, _P, _P]),
     "zv_text_condition": (_I, [_P, _P, _I, _I, _P, _P, _I, _P, _P]),
     "zv_speech_condition": (_I, [_P, _P, _I, _I, _I, _P, _I, _P, _P]),
+    # vocoder (zipvoice_amd/vocoder.py)
+    "zv_vocoder_create": (_P, [_P]),
+    "zv_vocoder_destroy": (None, [_P]),
+    "zv_vocoder_set_weight": (_I, [_P, ctypes.c_char_p, _P, ctypes.c_int64]),
+    "zv_vocoder_finalize": (_I, [_P]),
+    "zv_vocoder_decode": (_I, [_P, _P, _I, _F, _F, _P, _I, _I, _P, _I, _P]),
+    "zv_vocoder_device_bytes": (ctypes.c_int64, [_P]),
 }
 
 _lib = None
