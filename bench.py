@@ -43,6 +43,7 @@ HOP = 256
 BF16_DENSE_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16
 FP32_MFMA_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
+TRAFFIC_FILE = "r01_gemm_traffic.json"   # written by tools/pmc_traffic.py (tools/gpu/full.sh)
 
 
 def make_inputs(rank, device):
@@ -124,9 +125,18 @@ def roofline(model, vocoder, inp):
     total_ms = sum(v["ms"] for v in rep.values())
     achieved = r["flops"] / (r["ms"] * 1e-3) / 1e12
     peak = BF16_DENSE_PEAK_TFLOPS if name.endswith("bf16") else FP32_MFMA_PEAK_TFLOPS
+    traffic, tsrc = None, None
+    tpath = os.path.join(REPO, "profiles", TRAFFIC_FILE)
+    if name == "gemm_bf16" and os.path.exists(tpath):
+        with open(tpath) as f:
+            t = json.load(f)
+        traffic = t.get("traffic_bytes_per_launch")
+        tsrc = (f"profiles/{TRAFFIC_FILE}: rocprofv3 PMC FETCH_SIZE(x2, gfx950) + WRITE_SIZE "
+                f"per launch of {t['kernel_regex']} over one guided forward")
     return {
         "kernel": name, "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
-        "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+        "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+        "traffic_unit": "bytes per launch", "traffic_source": tsrc,
         "launches_per_step": r["launches"], "avg_launch_us": round(r["ms"] * 1e3 / r["launches"], 2),
         "flops_per_launch": r["flops"] / r["launches"],
         "share_of_profiled_time": round(r["ms"] / total_ms, 3),

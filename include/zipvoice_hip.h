@@ -33,6 +33,8 @@
  *                      `vocoder.decode(pred_features).squeeze(1).clamp(-1, 1)` with the
  *                      feature post-processing of infer_zipvoice.py:374-378
  *                      (third-party vocos 0.1.0: Vocos.decode = VocosBackbone + ISTFTHead)
+ *   zv_fbank_*         VocosFbank.extract (zipvoice/utils/feature.py:36-120): the prompt
+ *                      log-mel front end feeding prompt_features (infer_zipvoice.py:328-337)
  */
 #ifndef ZIPVOICE_HIP_H
 #define ZIPVOICE_HIP_H
@@ -175,6 +177,22 @@ int zv_vocoder_decode(zv_vocoder_handle v, const float* mel, int layout, float f
                       float feat_bias, const int32_t* lens, int B, int T, float* wav, int clamp,
                       void* stream);
 int64_t zv_vocoder_device_bytes(zv_vocoder_handle v);
+
+/* ------------------------------------------------------------------------
+ * Prompt feature extractor (VocosFbank: centred reflect-padded STFT, power 1,
+ * mel projection, log(clamp(1e-7)); fp32 arithmetic throughout).
+ * ---------------------------------------------------------------------- */
+typedef struct zv_fbank* zv_fbank_handle;
+/* host_window: [n_fft] analysis window (torch.hann_window, periodic);
+ * host_fb: [n_fft/2 + 1, n_mels] mel filterbank (torchaudio melscale_fbanks layout). */
+zv_fbank_handle zv_fbank_create(int n_fft, int hop, int n_mels, const float* host_window,
+                                const float* host_fb);
+void zv_fbank_destroy(zv_fbank_handle f);
+/* wav: [B, wav_ld] fp32 device samples, lens: [B] int32 sample counts (> n_fft/2);
+ * out: [B, T_out, out_ld] log-mel rows (columns [0, n_mels)); utterance b fills its
+ * first (lens[b] + hop/2) / hop rows (lhotse compute_num_frames), later rows are 0. */
+int zv_fbank_extract(zv_fbank_handle f, const float* wav, int64_t wav_ld, const int32_t* lens,
+                     int B, int T_out, float* out, int64_t out_ld, void* stream);
 
 #ifdef __cplusplus
 }

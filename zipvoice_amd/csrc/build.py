@@ -28,17 +28,23 @@ def up_to_date():
     return all(os.path.getmtime(d) <= t for d in DEPS)
 
 
-def build(force=False, verbose=True):
-    if not force and up_to_date():
+def build(force=False, verbose=True, out=None, defines=()):
+    if out is None and not force and up_to_date():
         return OUT
+    out = out or OUT
     cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-munsafe-fp-atomics", "-Wno-unused-result", "-o", OUT + ".tmp", SRC]
+           "-munsafe-fp-atomics", "-Wno-unused-result", *[f"-D{d}" for d in defines],
+           "-o", out + ".tmp", SRC]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    # build.py [--force] [--out PATH] [-DNAME ...]   (alternative builds for A/B runs)
+    args = sys.argv[1:]
+    out = args[args.index("--out") + 1] if "--out" in args else None
+    build(force="--force" in args, out=out,
+          defines=[a[2:] for a in args if a.startswith("-D")])

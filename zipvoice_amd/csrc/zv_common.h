@@ -32,20 +32,30 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // numerics (scaling.py formulas, fp32)
 // ---------------------------------------------------------------------------
 
+// Transcendentals of the fused GEMM / conv epilogues are written on the hardware
+// v_exp_f32 (2^x) / v_log_f32 (log2) / v_rcp_f32 forms (~1 ulp each): the libm
+// forms (__expf/__logf/tanhf) cost 20-44 VALU per element, which at K = 512 is
+// as long as the element's MFMA work.
+__device__ __forceinline__ float fast_exp(float x) {
+  return __builtin_amdgcn_exp2f(x * 1.44269504088896341f);
+}
+__device__ __forceinline__ float fast_ln(float x) {
+  return __builtin_amdgcn_logf(x) * 0.693147180559945309f;
+}
+
 // SwooshLForward, scaling.py:1174-1180: log(1+exp(x-4)) (x-4 if inf) - 0.08x - 0.035
-// (v_exp_f32 / v_log_f32 forms of the same formula: the GEMM epilogue runs it
-// on every hidden activation)
+// (exp overflows in fp32 for x-4 > 88.7; beyond 80 log(1+e^y) == y in fp32)
 __device__ __forceinline__ float swoosh_l(float x) {
-  float xo = x - 4.0f;
-  float ls = __logf(1.0f + __expf(xo));
-  if (isinf(ls)) ls = xo;
+  const float xo = x - 4.0f;
+  float ls = fast_ln(1.0f + fast_exp(xo));
+  ls = xo > 80.0f ? xo : ls;
   return ls - 0.08f * x - 0.035f;
 }
 // SwooshRForward, scaling.py:1185-1191
 __device__ __forceinline__ float swoosh_r(float x) {
-  float xo = x - 1.0f;
-  float ls = __logf(1.0f + __expf(xo));
-  if (isinf(ls)) ls = xo;
+  const float xo = x - 1.0f;
+  float ls = fast_ln(1.0f + fast_exp(xo));
+  ls = xo > 80.0f ? xo : ls;
   return ls - 0.08f * x - 0.313261687f;
 }
 // SwooshR module (SwooshRFunction without k2), scaling.py:1106-1116:
@@ -55,7 +65,15 @@ __device__ __forceinline__ float swoosh_r_lae(float x) {
   float m = fmaxf(y, 0.0f);
   return m + log1pf(expf(-fabsf(y))) - 0.08f * x - 0.313261687f;
 }
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+// torch.sigmoid (GLU gate): 1 / (1 + e^-x)
+__device__ __forceinline__ float sigmoidf_(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + fast_exp(-x));
+}
+// torch.tanh (NonlinAttention gate): 1 - 2 / (e^2x + 1); saturates to +-1 for |x| > 15
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float t = 1.0f - 2.0f * __builtin_amdgcn_rcpf(fast_exp(2.0f * x) + 1.0f);
+  return fabsf(x) > 15.0f ? copysignf(1.0f, x) : t;
+}
 
 template <typename T> __device__ __forceinline__ float to_f(T v);
 template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }

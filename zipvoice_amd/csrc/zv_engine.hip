@@ -147,6 +147,8 @@ struct zv_engine {
   Workspace ws_dec, ws_txt;
 
   bool materialize_attn = false;   // A/B: ZV_ATTN_MATERIALIZE=1 keeps the W-materialising path
+  int occ_plain = 1, occ_resid = 2, occ_fused = 1;   // GEMM waves/SIMD by epilogue class
+  int gridx_plain = 0, gridx_resid = 0, gridx_fused = 0;   // GEMM blocks per CU (0 = resident)
   int gemm_tile = 0;               // A/B: ZV_GEMM_TILE 0 = 128x128, 1 = 256x128, 2 = 256x256,
                                    // 3 = 256x128 3-stage (bf16 linears with N >= 256)
 
@@ -155,6 +157,16 @@ struct zv_engine {
     materialize_attn = e && e[0] == '1';
     const char* g = getenv("ZV_GEMM_TILE");
     gemm_tile = g ? atoi(g) : 0;
+    const char* o1 = getenv("ZV_GEMM_OCC_PLAIN");
+    const char* o2 = getenv("ZV_GEMM_OCC_RESID");
+    const char* o3 = getenv("ZV_GEMM_OCC_FUSED");
+    occ_plain = o1 ? atoi(o1) : 1;
+    occ_resid = o2 ? atoi(o2) : 2;
+    occ_fused = o3 ? atoi(o3) : 1;
+    auto envi = [](const char* k, int d) { const char* v = getenv(k); return v ? atoi(v) : d; };
+    gridx_plain = envi("ZV_GEMM_GRIDX_PLAIN", 0);
+    gridx_resid = envi("ZV_GEMM_GRIDX_RESID", 0);
+    gridx_fused = envi("ZV_GEMM_GRIDX_FUSED", 0);
   }
   ~zv_engine() {
     for (void* p : allocs) (void)hipFree(p);
@@ -472,7 +484,10 @@ struct zv_engine {
         return;
       }
     }
-    launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD>(p, 1, s, tag);
+    const bool occ2 = o.resid ? occ_resid == 2 : occ_plain == 2;
+    const int gx = o.resid ? gridx_resid : gridx_plain;
+    if (occ2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2>(p, 1, s, tag, true, gx);
+    else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1>(p, 1, s, tag, true, gx);
   }
 
   // ---------------------------------------------------------------- one layer
@@ -535,7 +550,8 @@ struct zv_engine {
       GemmParams p = gp_linear(W.na_in, cur_a, M);
       p.Ch = y.h; p.Cl = y.l; p.ldch = y.ld;
       p.Cth = xt.h; p.Ctl = xt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)hid * Lpad;
-      launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na");
+      if (occ_fused == 2) launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
+      else launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 1>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       Act nao = ws.na_o.get(M, round_up(hid, 64), split);
       if (materialize_attn) {
         GemmParams q{};
@@ -589,7 +605,8 @@ struct zv_engine {
       Act g = ws.glu.get(M, D, split);
       GemmParams p = gp_linear(W.conv_in[c], cur_a, M);
       p.Ch = g.h; p.Cl = g.l; p.ldch = g.ld; p.rowmask = pad;
-      launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu");
+      if (occ_fused == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
+      else launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 1>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       Act dw = ws.dw.get(M, D, split);
       launch_dwconv(g.h, g.l, g.ld, W.dw_w[c], W.dw_b[c], dw.h, dw.l, dw.ld, B, L, D, W.ks, s);
       linear<SPLIT>(W.conv_out[c], dw, M, res, s);
@@ -791,6 +808,7 @@ struct zv_engine {
 };
 
 #include "zv_vocoder.inc"
+#include "zv_fbank.inc"
 
 // ===========================================================================
 // C ABI
@@ -1082,6 +1100,33 @@ int zv_vocoder_decode(zv_vocoder_handle v, const float* mel, int layout, float f
     v->decode<3>(mel, layout, feat_scale, feat_bias, lens, B, T, wav, clamp, s);
   else
     v->decode<1>(mel, layout, feat_scale, feat_bias, lens, B, T, wav, clamp, s);
+  ZV_API_END
+}
+
+zv_fbank_handle zv_fbank_create(int n_fft, int hop, int n_mels, const float* host_window,
+                                const float* host_fb) {
+  zv_fbank* f = nullptr;
+  try {
+    ZV_REQUIRE(host_window && host_fb, "null window / filterbank");
+    f = new zv_fbank();
+    f->init(n_fft, hop, n_mels, host_window, host_fb);
+    return f;
+  } catch (const std::exception& e) {
+    delete f;
+    g_last_error = e.what();
+    return nullptr;
+  }
+}
+
+void zv_fbank_destroy(zv_fbank_handle f) { delete f; }
+
+int zv_fbank_extract(zv_fbank_handle f, const float* wav, int64_t wav_ld, const int32_t* lens,
+                     int B, int T_out, float* out, int64_t out_ld, void* stream) {
+  ZV_API_BEGIN
+  ZV_REQUIRE(f != nullptr, "null fbank handle");
+  ZV_REQUIRE(B > 0 && T_out > 0 && wav && lens && out, "bad arguments");
+  ZV_REQUIRE(out_ld >= f->n_mels, "out_ld < n_mels");
+  f->extract(wav, (long)wav_ld, lens, B, T_out, out, (long)out_ld, (hipStream_t)stream);
   ZV_API_END
 }
 

@@ -75,16 +75,22 @@ SIGNATURES = {
     "zv_vocoder_finalize": (_I, [_P]),
     "zv_vocoder_decode": (_I, [_P, _P, _I, _F, _F, _P, _I, _I, _P, _I, _P]),
     "zv_vocoder_device_bytes": (ctypes.c_int64, [_P]),
+    # prompt feature extractor (zipvoice_amd/feature.py)
+    "zv_fbank_create": (_P, [_I, _I, _I, _P, _P]),
+    "zv_fbank_destroy": (None, [_P]),
+    "zv_fbank_extract": (_I, [_P, _P, ctypes.c_int64, _P, _I, _I, _P, ctypes.c_int64, _P]),
 }
 
 _lib = None
 
 
-def load_library(path: str = LIB_PATH):
-    """dlopen the engine (fails loudly when it has not been built)."""
+def load_library(path: Optional[str] = None):
+    """dlopen the engine (fails loudly when it has not been built).  ZV_LIB_PATH
+    selects an alternative build of the same library (A/B measurements)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("ZV_LIB_PATH") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError(
             f"{LIB_NAME} not found at {path}: build it with "
@@ -92,6 +98,8 @@ def load_library(path: str = LIB_PATH):
             "There is no CPU fallback for the ZipVoice hot path.")
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in SIGNATURES.items():
+        if path != LIB_PATH and not hasattr(lib, name):
+            continue        # an older A/B build without this entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
