@@ -13,6 +13,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "zv_common.h"
@@ -70,6 +71,10 @@ struct ZipformerW {
   Linear te0, te2, guid;    // fp32 small linears
 };
 
+// bumped whenever a workspace buffer moves: captured HIP graphs bake in
+// workspace addresses and are dropped when it changes
+static unsigned long g_ws_generation = 0;
+
 // grow-only device buffer
 struct DBuf {
   void* p = nullptr;
@@ -77,6 +82,7 @@ struct DBuf {
   template <typename T> T* get(size_t n) {
     size_t need = n * sizeof(T) + 256;
     if (need > bytes) {
+      ++g_ws_generation;
       if (p) { ZV_CHECK(hipDeviceSynchronize()); ZV_CHECK(hipFree(p)); }
       ZV_CHECK(hipMalloc(&p, need));
       ZV_CHECK(hipMemset(p, 0, need));
@@ -147,28 +153,65 @@ struct zv_engine {
   Workspace ws_dec, ws_txt;
 
   bool materialize_attn = false;   // A/B: ZV_ATTN_MATERIALIZE=1 keeps the W-materialising path
-  int occ_plain = 1, occ_resid = 2, occ_fused = 1;   // GEMM waves/SIMD by epilogue class
-  int gridx_plain = 0, gridx_resid = 0, gridx_fused = 0;   // GEMM blocks per CU (0 = resident)
+  // GEMM launch policy by epilogue class (measured same-box, profiles/r01_gemm_policy_ab.txt):
+  // two 4-wave blocks per CU everywhere (OCC 2); the HBM-bound residual-stream linears
+  // one tile per block (gridx -1), the others persistent over the resident grid (0).
+  int occ_plain = 2, occ_resid = 2, occ_fused = 2;
+  int gridx_plain = 0, gridx_resid = -1, gridx_fused = 0;
   int gemm_tile = 0;               // A/B: ZV_GEMM_TILE 0 = 128x128, 1 = 256x128, 2 = 256x256,
                                    // 3 = 256x128 3-stage (bf16 linears with N >= 256)
 
   explicit zv_engine(const zv_config& c) : cfg(c) {
     const char* e = getenv("ZV_ATTN_MATERIALIZE");
     materialize_attn = e && e[0] == '1';
+    const char* gr = getenv("ZV_GRAPH");
+    graphs_enabled = !(gr && gr[0] == '0');
     const char* g = getenv("ZV_GEMM_TILE");
     gemm_tile = g ? atoi(g) : 0;
     const char* o1 = getenv("ZV_GEMM_OCC_PLAIN");
     const char* o2 = getenv("ZV_GEMM_OCC_RESID");
     const char* o3 = getenv("ZV_GEMM_OCC_FUSED");
-    occ_plain = o1 ? atoi(o1) : 1;
+    occ_plain = o1 ? atoi(o1) : 2;
     occ_resid = o2 ? atoi(o2) : 2;
-    occ_fused = o3 ? atoi(o3) : 1;
+    occ_fused = o3 ? atoi(o3) : 2;
     auto envi = [](const char* k, int d) { const char* v = getenv(k); return v ? atoi(v) : d; };
     gridx_plain = envi("ZV_GEMM_GRIDX_PLAIN", 0);
-    gridx_resid = envi("ZV_GEMM_GRIDX_RESID", 0);
+    gridx_resid = envi("ZV_GEMM_GRIDX_RESID", -1);
     gridx_fused = envi("ZV_GEMM_GRIDX_FUSED", 0);
   }
+  // ---------------------------------------------------------------- HIP graphs
+  // The whole N-step Euler solve (~250 launches per step) is captured once per
+  // (shape, schedule) on an engine-owned stream over engine-owned staging copies
+  // of the inputs, then replayed with one hipGraphLaunch: the host launch cost
+  // (which bounds small-batch / single-sentence latency) goes away.  The first
+  // call of a key runs uncaptured (it sizes the workspace and fills the
+  // positional caches, which synchronise); ZV_GRAPH=0 disables capture.
+  struct GraphKey {
+    int B, T, N, has_pad;
+    float g, t0, t1, shift;
+    unsigned long gen;
+    bool operator<(const GraphKey& o) const {
+      return std::tie(B, T, N, has_pad, g, t0, t1, shift, gen) <
+             std::tie(o.B, o.T, o.N, o.has_pad, o.g, o.t0, o.t1, o.shift, o.gen);
+    }
+  };
+  std::map<GraphKey, hipGraphExec_t> graphs;
+  std::map<GraphKey, int> graph_seen;
+  hipStream_t gstream = nullptr;
+  hipEvent_t gev_in = nullptr, gev_out = nullptr;
+  DBuf gx, gtc, gsc, gpad;
+  bool graphs_enabled = true;
+
+  void drop_graphs() {
+    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+    graphs.clear();
+  }
+
   ~zv_engine() {
+    drop_graphs();
+    if (gstream) (void)hipStreamDestroy(gstream);
+    if (gev_in) (void)hipEventDestroy(gev_in);
+    if (gev_out) (void)hipEventDestroy(gev_out);
     for (void* p : allocs) (void)hipFree(p);
     for (auto& kv : pe_cache) (void)hipFree(kv.second);
     for (auto& kv : posp_cache) (void)hipFree(kv.second);
@@ -773,6 +816,71 @@ struct zv_engine {
     }
   }
 
+  void euler_loop(float* x, const float* tc, const float* sc, const uint8_t* pad, int B, int T,
+                  const std::vector<float>& ts, float g, hipStream_t s) {
+    const int num_step = (int)ts.size() - 1;
+    for (int k = 0; k < num_step; ++k)
+      velocity(ts[k], g, x, tc, sc, pad, B, T, nullptr, true, ts[k + 1] - ts[k], s);
+  }
+
+  // zv_euler_sample body: graph replay when possible, plain launches otherwise
+  void euler_sample(float* x, const float* tc, const float* sc, const uint8_t* pad, int B, int T,
+                    int num_step, float g, float t0, float t1, float shift, hipStream_t s) {
+    const std::vector<float> ts = time_steps(t0, t1, num_step, shift);
+    if (!graphs_enabled || g_zv_prof.on) {
+      euler_loop(x, tc, sc, pad, B, T, ts, g, s);
+      return;
+    }
+    const int Fx = stereo() ? 2 * cfg.feat_dim : cfg.feat_dim;
+    const size_t nx = (size_t)B * T * Fx, nt = (size_t)B * T * cfg.feat_dim;
+    // staging buffers first (they count towards the workspace generation)
+    float* sx = gx.get<float>(nx);
+    float* stc = gtc.get<float>(nt);
+    float* ssc = gsc.get<float>(nx);
+    uint8_t* spad = pad ? gpad.get<uint8_t>((size_t)B * T) : nullptr;
+    GraphKey key{B, T, num_step, pad ? 1 : 0, g, t0, t1, shift, g_ws_generation};
+    auto it = graphs.find(key);
+    if (it == graphs.end() && graph_seen[key] == 0) {
+      graph_seen[key] = 1;                       // warm-up: sizes workspace, fills caches
+      euler_loop(x, tc, sc, pad, B, T, ts, g, s);
+      return;
+    }
+    if (!gstream) {
+      ZV_CHECK(hipStreamCreateWithFlags(&gstream, hipStreamNonBlocking));
+      ZV_CHECK(hipEventCreateWithFlags(&gev_in, hipEventDisableTiming));
+      ZV_CHECK(hipEventCreateWithFlags(&gev_out, hipEventDisableTiming));
+    }
+    ZV_CHECK(hipEventRecord(gev_in, s));
+    ZV_CHECK(hipStreamWaitEvent(gstream, gev_in, 0));
+    ZV_CHECK(hipMemcpyAsync(sx, x, nx * 4, hipMemcpyDeviceToDevice, gstream));
+    ZV_CHECK(hipMemcpyAsync(stc, tc, nt * 4, hipMemcpyDeviceToDevice, gstream));
+    ZV_CHECK(hipMemcpyAsync(ssc, sc, nx * 4, hipMemcpyDeviceToDevice, gstream));
+    if (pad) ZV_CHECK(hipMemcpyAsync(spad, pad, (size_t)B * T, hipMemcpyDeviceToDevice, gstream));
+    if (it == graphs.end()) {
+      if (key.gen != g_ws_generation) drop_graphs();
+      hipGraph_t graph = nullptr;
+      ZV_CHECK(hipStreamBeginCapture(gstream, hipStreamCaptureModeThreadLocal));
+      const unsigned long gen0 = g_ws_generation;
+      try {
+        euler_loop(sx, stc, ssc, spad, B, T, ts, g, gstream);
+      } catch (...) {
+        (void)hipStreamEndCapture(gstream, &graph);
+        if (graph) (void)hipGraphDestroy(graph);
+        throw;
+      }
+      ZV_CHECK(hipStreamEndCapture(gstream, &graph));
+      ZV_REQUIRE(gen0 == g_ws_generation, "workspace moved during graph capture");
+      hipGraphExec_t exec = nullptr;
+      ZV_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+      ZV_CHECK(hipGraphDestroy(graph));
+      it = graphs.emplace(key, exec).first;
+    }
+    ZV_CHECK(hipGraphLaunch(it->second, gstream));
+    ZV_CHECK(hipMemcpyAsync(x, sx, nx * 4, hipMemcpyDeviceToDevice, gstream));
+    ZV_CHECK(hipEventRecord(gev_out, gstream));
+    ZV_CHECK(hipStreamWaitEvent(s, gev_out, 0));
+  }
+
   static std::vector<float> time_steps(float t_start, float t_end, int num_step, float t_shift) {
     // torch.linspace float32 (forward half / backward half) + shift, solver.py:256-281
     const int steps = num_step + 1;
@@ -1017,10 +1125,8 @@ int zv_euler_sample(zv_handle h, float* x, const float* text_c, const float* spe
   ZV_API_BEGIN
   check_ready(h);
   ZV_REQUIRE(B > 0 && T > 0 && num_step > 0, "empty batch or zero steps");
-  const std::vector<float> ts = zv_engine::time_steps(t_start, t_end, num_step, t_shift);
-  for (int k = 0; k < num_step; ++k)
-    h->velocity(ts[k], guidance_scale, x, text_c, speech_c, pad, B, T, nullptr, true,
-                ts[k + 1] - ts[k], (hipStream_t)stream);
+  h->euler_sample(x, text_c, speech_c, pad, B, T, num_step, guidance_scale, t_start, t_end,
+                  t_shift, (hipStream_t)stream);
   ZV_API_END
 }
 
