@@ -103,6 +103,11 @@ int zv_profile_report(char* buf, int buflen);
  * (C += ..., fp32, plus a bf16 copy), 3 = SwooshL -> bf16. */
 int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, float* ms_out);
 
+/* GEMM self-check (test infrastructure): tile variant `variant` (20-23: the
+ * 256x256 phased kernel) against the 128x128 kernel on the same random operands,
+ * fp32 C; mode 0 plain, 1 SwooshL, 2 residual.  Writes max |diff| and max |ref|. */
+int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff, float* maxref);
+
 /* Raw decoder: v = fm_decoder(cat[xt, text_c, speech_c], t, pad, g).
  *  t:      [N] timesteps;  guidance: [N] (distill only, else NULL)
  *  xt, speech_c: [N, T, Fx]; text_c: [N, T, feat_dim]; pad: [N, T] uint8 (1 = padded) or NULL

@@ -35,11 +35,11 @@ if cur:
     recs.append(cur)
 dem = subprocess.run(["c++filt"], input="\n".join(r.get("name", "?") for r in recs), text=True,
                      capture_output=True).stdout.splitlines()
-print(f"{'kernel':70s} {'vgpr':>5s} {'agpr':>5s} {'sgpr':>5s} {'lds':>7s} {'spill':>5s}")
+print(f"{'kernel':70s} {'vgpr':>5s} {'agpr':>5s} {'sgpr':>5s} {'lds':>7s} {'spill':>5s} {'scratch':>7s}")
 for r, n in zip(recs, dem):
     n = n.split("(")[0]
     if pat and not pat.search(n):
         continue
     print(f"{n[:70]:70s} {r.get('vgpr_count','?'):>5s} {r.get('agpr_count','?'):>5s} "
           f"{r.get('sgpr_count','?'):>5s} {r.get('group_segment_fixed_size','?'):>7s} "
-          f"{r.get('vgpr_spill_count','?'):>5s}")
+          f"{r.get('vgpr_spill_count','?'):>5s} {r.get('private_segment_fixed_size','?'):>7s}")

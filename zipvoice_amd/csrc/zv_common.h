@@ -6,6 +6,8 @@
 #include <algorithm>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
+#include <utility>
 
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -143,3 +145,13 @@ struct ZvProfScope {
     }
   }
 };
+
+// compile-time loop: f(std::integral_constant<int, 0>) ... f(<N-1>)
+template <class F, int... Is>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}

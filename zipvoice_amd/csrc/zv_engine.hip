@@ -18,6 +18,7 @@
 
 #include "zv_common.h"
 #include "zv_gemm.inc"
+#include "zv_gemm8.inc"
 #include "zv_attn.inc"
 #include "zv_elem.inc"
 #include "zv_flash.inc"
@@ -948,14 +949,29 @@ static __global__ void zv_fill_rand_bf16(bf16* p, long n, unsigned seed) {
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int STAGES>
+template <int BM, int BN, int WGM, int WGN, int STAGES, int BK = GEMM_BK>
 static float bench_variant(GemmParams p, int iters, bool persistent, hipStream_t s) {
   hipEvent_t e0, e1;
   ZV_CHECK(hipEventCreate(&e0)); ZV_CHECK(hipEventCreate(&e1));
-  launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES>(p, 1, s, "bench", persistent);
+  launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES, 2, BK>(p, 1, s, "bench", persistent);
   ZV_CHECK(hipEventRecord(e0, s));
   for (int i = 0; i < iters; ++i)
-    launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES>(p, 1, s, "bench", persistent);
+    launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES, 2, BK>(p, 1, s, "bench", persistent);
+  ZV_CHECK(hipEventRecord(e1, s));
+  ZV_CHECK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  ZV_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  ZV_CHECK(hipEventDestroy(e0)); ZV_CHECK(hipEventDestroy(e1));
+  return ms / iters;
+}
+
+template <int ORDER, bool PB>
+static float bench_variant8(GemmParams p, int iters, hipStream_t s) {
+  hipEvent_t e0, e1;
+  ZV_CHECK(hipEventCreate(&e0)); ZV_CHECK(hipEventCreate(&e1));
+  launch_gemm8<ORDER, EPI_STD, PB>(p, s, "bench");
+  ZV_CHECK(hipEventRecord(e0, s));
+  for (int i = 0; i < iters; ++i) launch_gemm8<ORDER, EPI_STD, PB>(p, s, "bench");
   ZV_CHECK(hipEventRecord(e1, s));
   ZV_CHECK(hipEventSynchronize(e1));
   float ms = 0.f;
@@ -1067,6 +1083,7 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
   p.C = C; p.ldc = N; p.Ch = Ch; p.ldch = N; p.rows_per_group = 1; p.rpb = 1;
   if (out_mode == 2) p.resid = C;
   if (out_mode == 3) p.act = 1;
+  if (out_mode == 4) { p.C = nullptr; p.Ch = nullptr; }
   float ms = -1.f;
   switch (variant) {
     case 0: ms = bench_variant<128, 128, 2, 2, 2>(p, iters, persistent, s); break;
@@ -1080,12 +1097,86 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
     case 8: ms = bench_variant<256, 256, 2, 4, 2>(p, iters, persistent, s); break;
     case 9: ms = bench_variant<256, 128, 2, 4, 2>(p, iters, persistent, s); break;
     case 10: ms = bench_variant<128, 256, 1, 4, 2>(p, iters, persistent, s); break;
+    case 30: ms = bench_variant<128, 128, 2, 2, 4, 32>(p, iters, persistent, s); break;
+    case 31: ms = bench_variant<128, 128, 2, 2, 3, 32>(p, iters, persistent, s); break;
+    case 20: ms = bench_variant8<0, true>(p, iters, s); break;
+    case 21: ms = bench_variant8<1, true>(p, iters, s); break;
+    case 22: ms = bench_variant8<0, false>(p, iters, s); break;
+    case 23: ms = bench_variant8<1, false>(p, iters, s); break;
     default: throw std::invalid_argument("unknown variant");
   }
   *ms_out = ms;
   ZV_CHECK(hipFree(A)); ZV_CHECK(hipFree(W));
   if (C) ZV_CHECK(hipFree(C));
   if (Ch) ZV_CHECK(hipFree(Ch));
+  ZV_API_END
+}
+
+// GEMM self-check: variant (bench ids) against the 128x128 kernel on the same
+// random operands, fp32 C (+ optional residual / SwooshL epilogue).  Writes the
+// max |diff| and the max |ref|.
+static __global__ void zv_zero_kpad_kernel(bf16* p, long rows, int ld, int K) {
+  const long n = rows * (long)(ld - K);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    p[(i / (ld - K)) * ld + K + i % (ld - K)] = (bf16)0.f;
+}
+static __global__ void zv_maxdiff_kernel(const float* a, const float* b, long n, float* out) {
+  float d = 0.f, r = 0.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    d = fmaxf(d, fabsf(a[i] - b[i]));
+    r = fmaxf(r, fabsf(b[i]));
+  }
+  atomicMax(reinterpret_cast<int*>(out), __float_as_int(d));
+  atomicMax(reinterpret_cast<int*>(out + 1), __float_as_int(r));
+}
+
+int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff, float* maxref) {
+  ZV_API_BEGIN
+  hipStream_t s = nullptr;
+  const long Kp = round_up(K, 64), Np = round_up(N, 256);
+  bf16 *A, *W;
+  float *C0, *C1, *R, *res;
+  ZV_CHECK(hipMalloc(&A, (size_t)M * Kp * 2));
+  ZV_CHECK(hipMalloc(&W, (size_t)Np * Kp * 2));
+  ZV_CHECK(hipMalloc(&C0, (size_t)M * N * 4));
+  ZV_CHECK(hipMalloc(&C1, (size_t)M * N * 4));
+  ZV_CHECK(hipMalloc(&R, (size_t)M * N * 4));
+  ZV_CHECK(hipMalloc(&res, 8));
+  hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(4096), dim3(256), 0, s, A, (long)M * Kp, 1u);
+  hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(4096), dim3(256), 0, s, W, (long)Np * Kp, 2u);
+  hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(4096), dim3(256), 0, s, reinterpret_cast<bf16*>(R),
+                     (long)M * N * 2, 3u);   // finite garbage as the residual
+  if (Kp > K) {   // the engine's operands are zero beyond K (padded to the K step)
+    hipLaunchKernelGGL(zv_zero_kpad_kernel, dim3(1024), dim3(256), 0, s, A, (long)M, (int)Kp, K);
+    hipLaunchKernelGGL(zv_zero_kpad_kernel, dim3(1024), dim3(256), 0, s, W, (long)Np, (int)Kp, K);
+  }
+  GemmParams p{};
+  p.M = M; p.N = N; p.K = K; p.nz2 = 1; p.Brows = (int)Np;
+  p.Ah = A; p.lda = Kp; p.Bh = W; p.ldb = Kp; p.ldc = N; p.rows_per_group = 1; p.rpb = 1;
+  if (mode == 1) p.act = 1;
+  float* outs[2] = {C0, C1};
+  for (int k = 0; k < 2; ++k) {
+    p.C = outs[k];
+    if (mode == 2) {
+      ZV_CHECK(hipMemcpyAsync(outs[k], R, (size_t)M * N * 4, hipMemcpyDeviceToDevice, s));
+      p.resid = outs[k];
+    }
+    if (k == 0) launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2>(p, 1, s, "ref", true, 0);
+    else switch (variant) {
+      case 30: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 4, 2, 32>(p, 1, s, "t", true, 0); break;
+      case 20: launch_gemm8<0, EPI_STD, true>(p, s, "t"); break;
+      case 21: launch_gemm8<1, EPI_STD, true>(p, s, "t"); break;
+      case 22: launch_gemm8<0, EPI_STD, false>(p, s, "t"); break;
+      case 23: launch_gemm8<1, EPI_STD, false>(p, s, "t"); break;
+      default: throw std::invalid_argument("selftest: unknown variant");
+    }
+  }
+  ZV_CHECK(hipMemsetAsync(res, 0, 8, s));
+  hipLaunchKernelGGL(zv_maxdiff_kernel, dim3(1024), dim3(256), 0, s, C1, C0, (long)M * N, res);
+  float h[2];
+  ZV_CHECK(hipMemcpy(h, res, 8, hipMemcpyDeviceToHost));
+  *maxdiff = h[0]; *maxref = h[1];
+  for (void* q : {(void*)A, (void*)W, (void*)C0, (void*)C1, (void*)R, (void*)res}) ZV_CHECK(hipFree(q));
   ZV_API_END
 }
 

@@ -61,6 +61,7 @@ SIGNATURES = {
     "zv_device_bytes": (ctypes.c_int64, [_P]),
     "zv_profile": (_I, [_I]),
     "zv_bench_gemm": (_I, [_I, _I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_float)]),
+    "zv_gemm_selftest": (_I, [_I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "zv_profile_report": (_I, [ctypes.c_char_p, _I]),
     "zv_fm_decoder": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
     "zv_velocity": (_I, [_P, _F, _F, _P, _P, _P, _P, _I, _I, _P, _P]),
