@@ -159,8 +159,13 @@ struct zv_engine {
   // one tile per block (gridx -1), the others persistent over the resident grid (0).
   int occ_plain = 2, occ_resid = 2, occ_fused = 2;
   int gridx_plain = 0, gridx_resid = -1, gridx_fused = 0;
-  int gemm_tile = 0;               // A/B: ZV_GEMM_TILE 0 = 128x128, 1 = 256x128, 2 = 256x256,
-                                   // 3 = 256x128 3-stage (bf16 linears with N >= 256)
+  int fused_tile = 0;              // A/B: ZV_GEMM_FUSED_TILE 1 = GLU / NA in-projections on
+                                   // 256-row 3-stage tiles (one 8-wave block per CU)
+  int gemm_tile = 0;               // ZV_GEMM_TILE 0 (default): 128x128 two blocks per CU; A/B arms
+                                   // (bf16 linears with N >= 256): 1 = 256x128, 2 = 256x256,
+                                   // 3 = 256x128 3-stage, 5 = 256x128 3-stage for the
+                                   // non-residual ones only (same-box in-model A/B within noise:
+                                   // profiles/r01_gemm_tile_ab.txt)
 
   explicit zv_engine(const zv_config& c) : cfg(c) {
     const char* e = getenv("ZV_ATTN_MATERIALIZE");
@@ -179,6 +184,7 @@ struct zv_engine {
     gridx_plain = envi("ZV_GEMM_GRIDX_PLAIN", 0);
     gridx_resid = envi("ZV_GEMM_GRIDX_RESID", -1);
     gridx_fused = envi("ZV_GEMM_GRIDX_FUSED", 0);
+    fused_tile = envi("ZV_GEMM_FUSED_TILE", 0);
   }
   // ---------------------------------------------------------------- HIP graphs
   // The whole N-step Euler solve (~250 launches per step) is captured once per
@@ -528,6 +534,12 @@ struct zv_engine {
         return;
       }
     }
+    if constexpr (SPLIT == 1) {
+      if (gemm_tile == 5 && !o.resid && Lw.N >= 256) {
+        launch_gemm<256, 128, 4, 2, SPLIT, EPI_STD, 3>(p, 1, s, tag);
+        return;
+      }
+    }
     const bool occ2 = o.resid ? occ_resid == 2 : occ_plain == 2;
     const int gx = o.resid ? gridx_resid : gridx_plain;
     if (occ2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2>(p, 1, s, tag, true, gx);
@@ -594,7 +606,11 @@ struct zv_engine {
       GemmParams p = gp_linear(W.na_in, cur_a, M);
       p.Ch = y.h; p.Cl = y.l; p.ldch = y.ld;
       p.Cth = xt.h; p.Ctl = xt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)hid * Lpad;
-      if (occ_fused == 2) launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
+      bool done = false;
+      if constexpr (SPLIT == 1)
+        if (fused_tile == 1) { launch_gemm<256, 96, 4, 2, SPLIT, EPI_NA, 2, 2>(p, 1, s, "gemm_bf16_na"); done = true; }
+      if (done) {}
+      else if (occ_fused == 2) launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       else launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 1>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       Act nao = ws.na_o.get(M, round_up(hid, 64), split);
       if (materialize_attn) {
@@ -649,7 +665,11 @@ struct zv_engine {
       Act g = ws.glu.get(M, D, split);
       GemmParams p = gp_linear(W.conv_in[c], cur_a, M);
       p.Ch = g.h; p.Cl = g.l; p.ldch = g.ld; p.rowmask = pad;
-      if (occ_fused == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
+      bool done = false;
+      if constexpr (SPLIT == 1)
+        if (fused_tile == 1) { launch_gemm<256, 128, 4, 2, SPLIT, EPI_GLU, 3>(p, 1, s, "gemm_bf16_glu"); done = true; }
+      if (done) {}
+      else if (occ_fused == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       else launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 1>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       Act dw = ws.dw.get(M, D, split);
       launch_dwconv(g.h, g.l, g.ld, W.dw_w[c], W.dw_b[c], dw.h, dw.l, dw.ld, B, L, D, W.ks, s);
@@ -663,7 +683,10 @@ struct zv_engine {
     }
     self_attn(1);                                     // SA2 (+ temb)
     conv(1);                                          // conv2
-    ff(2, res);                                       // FF3
+    {                                                 // FF3: only the fp32 stream feeds BiasNorm
+      Out e = res; e.act = Act{};                     // (which rewrites both copies): no bf16 copy
+      ff(2, e);
+    }
     // BiasNorm + bypass -> src; next layer's working copy (src + temb) -> cur
     hipLaunchKernelGGL(zv_biasnorm_bypass_kernel, dim3(cdiv(M, 4)), dim3(256), 0, s, cur, src,
                        W.norm_bias, W.norm_log_scale, W.bypass, src, src_a.h, src_a.l,
