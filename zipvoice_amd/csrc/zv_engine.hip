@@ -159,6 +159,8 @@ struct zv_engine {
   // one tile per block (gridx -1), the others persistent over the resident grid (0).
   int occ_plain = 2, occ_resid = 2, occ_fused = 2;
   int gridx_plain = 0, gridx_resid = -1, gridx_fused = 0;
+  bool sa_pos_mfma = false;        // A/B: ZV_SA_POS_MFMA=1 puts the SelfAttention positional term on
+                                   // f32 MFMA (parity-green, same time: the loop is latency bound)
   int fused_tile = 0;              // A/B: ZV_GEMM_FUSED_TILE 1 = GLU / NA in-projections on
                                    // 256-row 3-stage tiles (one 8-wave block per CU)
   int gemm_tile = 0;               // ZV_GEMM_TILE 0 (default): 128x128 two blocks per CU; A/B arms
@@ -185,6 +187,7 @@ struct zv_engine {
     gridx_resid = envi("ZV_GEMM_GRIDX_RESID", -1);
     gridx_fused = envi("ZV_GEMM_GRIDX_FUSED", 0);
     fused_tile = envi("ZV_GEMM_FUSED_TILE", 0);
+    sa_pos_mfma = envi("ZV_SA_POS_MFMA", 0) != 0;
   }
   // ---------------------------------------------------------------- HIP graphs
   // The whole N-step Euler solve (~250 launches per step) is captured once per
@@ -655,7 +658,8 @@ struct zv_engine {
         f.vh = vt.h; f.vl = vt.l; f.ldv = Lpad; f.sv_b = (long)HV * Lpad; f.vrows_per_head = vd;
         f.nv = vd;
         f.oh = o.h; f.ol = o.l; f.ldo = o.ld; f.ocol_per_head = vd;
-        launch_attn_sa<SPLIT>(f, s);
+        if (sa_pos_mfma) launch_attn_sa_mf<SPLIT>(f, s);
+        else launch_attn_sa<SPLIT>(f, s);
       }
       Out e = res;
       if (temb) { e.rowvec = temb; e.rowvec_ld = D; e.rows_per_group = L; }
