@@ -161,6 +161,9 @@ struct zv_engine {
   int gridx_plain = 0, gridx_resid = -1, gridx_fused = 0;
   bool sa_pos_mfma = false;        // A/B: ZV_SA_POS_MFMA=1 puts the SelfAttention positional term on
                                    // f32 MFMA (parity-green, same time: the loop is latency bound)
+  bool skinny_tiles = true;        // V^T projection (N = 48) on 64x64 tiles, one per block
+                                   // (ZV_GEMM_SKINNY=0: 128x64 persistent arm; a 128x96 tile for
+                                   // the N = 272 projection measured slower: profiles/r01_skinny_ab.txt)
   int fused_tile = 0;              // A/B: ZV_GEMM_FUSED_TILE 1 = GLU / NA in-projections on
                                    // 256-row 3-stage tiles (one 8-wave block per CU)
   int gemm_tile = 0;               // ZV_GEMM_TILE 0 (default): 128x128 two blocks per CU; A/B arms
@@ -188,6 +191,7 @@ struct zv_engine {
     gridx_fused = envi("ZV_GEMM_GRIDX_FUSED", 0);
     fused_tile = envi("ZV_GEMM_FUSED_TILE", 0);
     sa_pos_mfma = envi("ZV_SA_POS_MFMA", 0) != 0;
+    skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
   }
   // ---------------------------------------------------------------- HIP graphs
   // The whole N-step Euler solve (~250 launches per step) is captured once per
@@ -644,7 +648,9 @@ struct zv_engine {
       Act o = ws.sa_o.get(M, 64, split);
       GemmParams p = gp_linear(W.sa_in[a], cur_a, M);
       p.Cth = vt.h; p.Ctl = vt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)HV * Lpad;
-      launch_gemm<128, 64, 2, 2, SPLIT, EPI_TRANS>(p, 1, s, split ? "gemm_fp32_t" : "gemm_bf16_t");
+      // N = 48: 64-row tiles give 2x the blocks of a 128-row grid (one tile column)
+      if (skinny_tiles) launch_gemm<64, 64, 2, 2, SPLIT, EPI_TRANS>(p, 1, s, split ? "gemm_fp32_t" : "gemm_bf16_t", true, -1);
+      else launch_gemm<128, 64, 2, 2, SPLIT, EPI_TRANS>(p, 1, s, split ? "gemm_fp32_t" : "gemm_bf16_t");
       if (materialize_attn) {
         GemmParams q{};
         q.M = L; q.N = vd; q.K = L; q.nz2 = B; q.Brows = vd;
