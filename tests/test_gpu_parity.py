@@ -159,3 +159,25 @@ def test_materialized_attention_path_matches(monkeypatch):
     check(v_mat, d["v"], "fp32", "decoder_fwd (materialised W)")
     v_fused = model("zipvoice", "fp32").forward_fm_decoder(**args)
     assert (v_mat - v_fused).abs().max().item() < 1e-4
+
+
+def test_dialog_long_sequence_fused_vs_materialized():
+    """Config C4 length (30 s dialogue: T = 3376 frames, the longest attention the
+    benchmark configs reach) on a ragged batch of two with a padded second item:
+    the production bf16 path (fused flash-style attention consumers) against the
+    fp32-accurate mode, whose fused images do not fit LDS at this length and which
+    therefore runs the W-materialising attention (an independent implementation of
+    the same softmax).  Bar: the bf16 tolerance of this file."""
+    rng = np.random.default_rng(11)
+    B, T = 2, 3376
+    x = cuda(rng.standard_normal((B, T, 100), dtype=np.float32))
+    tc = cuda(rng.standard_normal((B, T, 100), dtype=np.float32))
+    sc = cuda((0.3 * rng.standard_normal((B, T, 100)) - 0.5).astype(np.float32))
+    pm = cuda(np.arange(T)[None] >= np.array([T, 2901])[:, None])
+    args = dict(t=torch.tensor(0.6), xt=x, text_condition=tc, speech_condition=sc, padding_mask=pm)
+    fused = model("zipvoice_dialog", "bf16").forward_fm_decoder(**args)
+    ref = model("zipvoice_dialog", "fp32").forward_fm_decoder(**args)
+    valid = (~pm).cpu().numpy()
+    f = fused.float().cpu().numpy()[valid]
+    r = ref.float().cpu().numpy()[valid]
+    check(f, r, "bf16", f"dialog T={T} bf16 fused vs fp32 materialised")

@@ -583,11 +583,13 @@ struct zv_engine {
     const int qkpN = W.attn_in.N;
     Act qkp = ws.qkp.get(M, qkpN, split);
     { Out o; o.act = qkp; linear<SPLIT>(W.attn_in, src_a, M, o, s); }
-    // attention: either materialise W (reference structure, A/B path) or keep
-    // only per-row softmax statistics and recompute scores inside each consumer
+    // attention: either materialise W (reference structure; A/B path, and the
+    // fallback for lengths whose fused LDS images do not fit) or keep only
+    // per-row softmax statistics and recompute scores inside each consumer
+    const bool materialize = materialize_attn || !fused_attn_fits<SPLIT>(L, W.na_in.N / 3);
     Act Wt;
     FlashParams fp{};
-    if (materialize_attn) {
+    if (materialize) {
       Wt = ws.W.get((long)H * M, Lpad, split);
       AttnParams ap{qkp.h, qkp.l, qkpN, posP, pad, Wt.h, Wt.l, Lpad, B, L, H};
       launch_attn_softmax<SPLIT>(ap, s);
@@ -620,7 +622,7 @@ struct zv_engine {
       else if (occ_fused == 2) launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       else launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 1>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       Act nao = ws.na_o.get(M, round_up(hid, 64), split);
-      if (materialize_attn) {
+      if (materialize) {
         GemmParams q{};
         q.M = L; q.N = hid; q.K = L; q.nz2 = B; q.Brows = hid;
         q.Ah = Wt.h; q.Al = Wt.l; q.lda = Lpad; q.sA2 = (long)L * Lpad;     // head 0
@@ -651,7 +653,7 @@ struct zv_engine {
       // N = 48: 64-row tiles give 2x the blocks of a 128-row grid (one tile column)
       if (skinny_tiles) launch_gemm<64, 64, 2, 2, SPLIT, EPI_TRANS>(p, 1, s, split ? "gemm_fp32_t" : "gemm_bf16_t", true, -1);
       else launch_gemm<128, 64, 2, 2, SPLIT, EPI_TRANS>(p, 1, s, split ? "gemm_fp32_t" : "gemm_bf16_t");
-      if (materialize_attn) {
+      if (materialize) {
         GemmParams q{};
         q.M = L; q.N = vd; q.K = L; q.nz2 = B; q.Brows = vd;
         q.Ah = Wt.h; q.Al = Wt.l; q.lda = Lpad; q.sA1 = M * Lpad; q.sA2 = (long)L * Lpad;
