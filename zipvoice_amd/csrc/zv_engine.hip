@@ -523,8 +523,8 @@ struct zv_engine {
     p.resid = o.resid; p.rowvec = o.rowvec; p.rowvec_ld = o.rowvec_ld;
     p.rows_per_group = o.rows_per_group; p.orig = o.orig; p.byp = o.byp;
     const char* tag = SPLIT == 3 ? "gemm_fp32" : "gemm_bf16";
-    if (Lw.N <= 64) {
-      launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD>(p, 1, s, tag);
+    if (Lw.N <= 64) {   // own tag: the roofline's gemm_bf16 is the 128x128 instantiation alone
+      launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD>(p, 1, s, SPLIT == 3 ? "gemm_fp32_n64" : "gemm_bf16_n64");
       return;
     }
     if constexpr (SPLIT == 1) {
