@@ -19,7 +19,7 @@ if len(sys.argv) > 2:
 bad = 0
 for (M, N, K) in shapes:
     for v in variants:
-        for mode in (0, 1, 2):
+        for mode in ((0, 1) if v == 40 else (0, 1, 2)):
             d, r = ctypes.c_float(), ctypes.c_float()
             rc = lib.zv_gemm_selftest(M, N, K, v, mode, ctypes.byref(d), ctypes.byref(r))
             if rc:

@@ -164,6 +164,9 @@ struct zv_engine {
   bool skinny_tiles = true;        // V^T projection (N = 48) on 64x64 tiles, one per block
                                    // (ZV_GEMM_SKINNY=0: 128x64 persistent arm; a 128x96 tile for
                                    // the N = 272 projection measured slower: profiles/r01_skinny_ab.txt)
+  bool defer_stores = false;       // A/B: ZV_GEMM_DEFER=1 lets the next tile's K loop run past the
+                                   // plain bf16 linears' stores (bitwise equal; up to 6 % in isolation,
+                                   // ~1 % slower in the model: profiles/r01_gemm_defer_ab.txt)
   int fused_tile = 0;              // A/B: ZV_GEMM_FUSED_TILE 1 = GLU / NA in-projections on
                                    // 256-row 3-stage tiles (one 8-wave block per CU)
   int gemm_tile = 0;               // ZV_GEMM_TILE 0 (default): 128x128 two blocks per CU; A/B arms
@@ -192,6 +195,7 @@ struct zv_engine {
     fused_tile = envi("ZV_GEMM_FUSED_TILE", 0);
     sa_pos_mfma = envi("ZV_SA_POS_MFMA", 0) != 0;
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
+    defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
   }
   // ---------------------------------------------------------------- HIP graphs
   // The whole N-step Euler solve (~250 launches per step) is captured once per
@@ -544,6 +548,15 @@ struct zv_engine {
     if constexpr (SPLIT == 1) {
       if (gemm_tile == 5 && !o.resid && Lw.N >= 256) {
         launch_gemm<256, 128, 4, 2, SPLIT, EPI_STD, 3>(p, 1, s, tag);
+        return;
+      }
+    }
+    if constexpr (SPLIT == 1) {
+      // bf16-only outputs on whole tiles: the next tile's K loop does not wait for
+      // this tile's stores (counted vmcnt, zv_gemm.inc DEFER)
+      if (defer_stores && !o.resid && !o.C && o.act.h && !o.act.l && Lw.N % 128 == 0 &&
+          o.act.ld % 8 == 0 && occ_plain == 2) {
+        launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 8>(p, 1, s, tag, true, gridx_plain);
         return;
       }
     }
@@ -984,14 +997,14 @@ static __global__ void zv_fill_rand_bf16(bf16* p, long n, unsigned seed) {
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int STAGES, int BK = GEMM_BK>
+template <int BM, int BN, int WGM, int WGN, int STAGES, int BK = GEMM_BK, int DEFER = 0>
 static float bench_variant(GemmParams p, int iters, bool persistent, hipStream_t s) {
   hipEvent_t e0, e1;
   ZV_CHECK(hipEventCreate(&e0)); ZV_CHECK(hipEventCreate(&e1));
-  launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES, 2, BK>(p, 1, s, "bench", persistent);
+  launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES, 2, BK, DEFER>(p, 1, s, "bench", persistent);
   ZV_CHECK(hipEventRecord(e0, s));
   for (int i = 0; i < iters; ++i)
-    launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES, 2, BK>(p, 1, s, "bench", persistent);
+    launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES, 2, BK, DEFER>(p, 1, s, "bench", persistent);
   ZV_CHECK(hipEventRecord(e1, s));
   ZV_CHECK(hipEventSynchronize(e1));
   float ms = 0.f;
@@ -1133,6 +1146,7 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
     case 9: ms = bench_variant<256, 128, 2, 4, 2>(p, iters, persistent, s); break;
     case 10: ms = bench_variant<128, 256, 1, 4, 2>(p, iters, persistent, s); break;
     case 30: ms = bench_variant<128, 128, 2, 2, 4, 32>(p, iters, persistent, s); break;
+    case 40: ms = bench_variant<128, 128, 2, 2, 2, GEMM_BK, 8>(p, iters, persistent, s); break;
     case 31: ms = bench_variant<128, 128, 2, 2, 3, 32>(p, iters, persistent, s); break;
     case 20: ms = bench_variant8<0, true>(p, iters, s); break;
     case 21: ms = bench_variant8<1, true>(p, iters, s); break;
@@ -1154,6 +1168,10 @@ static __global__ void zv_zero_kpad_kernel(bf16* p, long rows, int ld, int K) {
   const long n = rows * (long)(ld - K);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     p[(i / (ld - K)) * ld + K + i % (ld - K)] = (bf16)0.f;
+}
+static __global__ void zv_bf16_to_f32_kernel(const bf16* a, float* b, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    b[i] = (float)a[i];
 }
 static __global__ void zv_maxdiff_kernel(const float* a, const float* b, long n, float* out) {
   float d = 0.f, r = 0.f;
@@ -1190,8 +1208,17 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
   p.Ah = A; p.lda = Kp; p.Bh = W; p.ldb = Kp; p.ldc = N; p.rows_per_group = 1; p.rpb = 1;
   if (mode == 1) p.act = 1;
   float* outs[2] = {C0, C1};
+  // the deferred-store variant writes bf16 only: both runs then write bf16 (into
+  // the two halves of R) and are widened into C0 / C1 for the comparison
+  const bool bf16_out = variant == 40;
+  if (bf16_out && mode == 2) throw std::invalid_argument("selftest: variant 40 has no residual form");
   for (int k = 0; k < 2; ++k) {
     p.C = outs[k];
+    if (bf16_out) {
+      p.C = nullptr;
+      p.Ch = reinterpret_cast<bf16*>(R) + (size_t)k * M * N;   // R (2 x M x N bf16) is free here
+      p.ldch = N;
+    }
     if (mode == 2) {
       ZV_CHECK(hipMemcpyAsync(outs[k], R, (size_t)M * N * 4, hipMemcpyDeviceToDevice, s));
       p.resid = outs[k];
@@ -1199,6 +1226,7 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
     if (k == 0) launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2>(p, 1, s, "ref", true, 0);
     else switch (variant) {
       case 30: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 4, 2, 32>(p, 1, s, "t", true, 0); break;
+      case 40: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2, GEMM_BK, 8>(p, 1, s, "t", true, 0); break;
       case 20: launch_gemm8<0, EPI_STD, true>(p, s, "t"); break;
       case 21: launch_gemm8<1, EPI_STD, true>(p, s, "t"); break;
       case 22: launch_gemm8<0, EPI_STD, false>(p, s, "t"); break;
@@ -1206,6 +1234,10 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
       default: throw std::invalid_argument("selftest: unknown variant");
     }
   }
+  if (bf16_out)
+    for (int k = 0; k < 2; ++k)
+      hipLaunchKernelGGL(zv_bf16_to_f32_kernel, dim3(1024), dim3(256), 0, s,
+                         reinterpret_cast<bf16*>(R) + (size_t)k * M * N, outs[k], (long)M * N);
   ZV_CHECK(hipMemsetAsync(res, 0, 8, s));
   hipLaunchKernelGGL(zv_maxdiff_kernel, dim3(1024), dim3(256), 0, s, C1, C0, (long)M * N, res);
   float h[2];
