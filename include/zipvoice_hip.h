@@ -33,7 +33,8 @@
  *                      `vocoder.decode(pred_features).squeeze(1).clamp(-1, 1)` with the
  *                      feature post-processing of infer_zipvoice.py:374-378
  *                      (third-party vocos 0.1.0: Vocos.decode = VocosBackbone + ISTFTHead)
- *   zv_fbank_*         VocosFbank.extract (zipvoice/utils/feature.py:36-120): the prompt
+ *   zv_fbank_*         VocosFbank.extract (zipvoice/utils/feature.py:36-120) and
+ *                      BigVGANFbank.extract (:133-204, _bigvgan_mel_feature.py:42-111): the prompt
  *                      log-mel front end feeding prompt_features (infer_zipvoice.py:328-337)
  */
 #ifndef ZIPVOICE_HIP_H
@@ -196,6 +197,13 @@ void zv_fbank_destroy(zv_fbank_handle f);
 /* wav: [B, wav_ld] fp32 device samples, lens: [B] int32 sample counts (> n_fft/2);
  * out: [B, T_out, out_ld] log-mel rows (columns [0, n_mels)); utterance b fills its
  * first (lens[b] + hop/2) / hop rows (lhotse compute_num_frames), later rows are 0. */
+/* Front-end variant (defaults: VocosFbank).  frame_offset = sample offset of frame
+ * 0 (n_fft/2: centred STFT; (n_fft - hop)/2: BigVGANFbank's explicit reflect pad +
+ * center=False), mag_eps added under the magnitude's square root (BigVGAN 1e-9),
+ * log_floor the clamp before the log (Vocos 1e-7, BigVGAN 1e-5).  Frames past the
+ * last STFT frame replicate it (BigVGANFbank's replicate pad to the lhotse count).
+ * Reference: zipvoice/utils/feature.py:133-204, _bigvgan_mel_feature.py:42-111. */
+int zv_fbank_configure(zv_fbank_handle f, int frame_offset, float mag_eps, float log_floor);
 int zv_fbank_extract(zv_fbank_handle f, const float* wav, int64_t wav_ld, const int32_t* lens,
                      int B, int T_out, float* out, int64_t out_ld, void* stream);
 

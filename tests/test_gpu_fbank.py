@@ -62,3 +62,37 @@ def test_extract_stereo_concatenates_channels():
     for c in range(2):
         ref = vocos_fbank(x[c], fx.window.numpy(), fx.fb.numpy())
         compare(got[:, c * 100:(c + 1) * 100].numpy(), ref)
+
+
+# ---- BigVGANFbank (feature.py:133-204): same kernel, BigVGAN framing / eps / floor
+
+def test_bigvgan_extract_matches_oracle_mono_and_replicate_tail():
+    from oracle.fbank_np import bigvgan_fbank
+    from zipvoice_amd.feature import BigVGANFbank
+    fx = BigVGANFbank()
+    for n, seed in ((24000 * 3 + 100, 3), (1000, 4)):   # 1000: last frame replicated
+        x = speechlike(n, seed)
+        got = fx.extract(x, 24000)
+        ref = bigvgan_fbank(x, fx.window.numpy(), fx.fb)
+        compare(got, ref)
+
+
+def test_bigvgan_batch_ragged_and_stereo():
+    from oracle.fbank_np import bigvgan_fbank
+    from zipvoice_amd.feature import BigVGANFbank
+    fx = BigVGANFbank()
+    lens = [24000 + 7, 24000 * 2 - 300, 5000]
+    wavs = np.zeros((3, max(lens)), np.float32)
+    for i, n in enumerate(lens):
+        wavs[i, :n] = speechlike(n, 10 + i)
+    feats, nfr = fx.extract_batch(torch.from_numpy(wavs).cuda(), torch.tensor(lens))
+    for i, n in enumerate(lens):
+        ref = bigvgan_fbank(wavs[i, :n], fx.window.numpy(), fx.fb)
+        assert int(nfr[i]) == ref.shape[0]
+        compare(feats[i, :ref.shape[0]].cpu().numpy(), ref)
+    st = BigVGANFbank(num_channels=2)
+    x2 = np.stack([speechlike(24000, 20), speechlike(24000, 21)])
+    got = st.extract(x2, 24000)
+    ref = np.concatenate([bigvgan_fbank(x2[0], st.window.numpy(), st.fb),
+                          bigvgan_fbank(x2[1], st.window.numpy(), st.fb)], axis=1)
+    compare(got, ref)

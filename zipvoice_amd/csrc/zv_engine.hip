@@ -1384,6 +1384,16 @@ zv_fbank_handle zv_fbank_create(int n_fft, int hop, int n_mels, const float* hos
 
 void zv_fbank_destroy(zv_fbank_handle f) { delete f; }
 
+int zv_fbank_configure(zv_fbank_handle f, int frame_offset, float mag_eps, float log_floor) {
+  ZV_API_BEGIN
+  ZV_REQUIRE(f != nullptr, "null fbank handle");
+  ZV_REQUIRE(frame_offset >= 0 && frame_offset <= f->n_fft / 2 && 2 * frame_offset >= f->n_fft - f->hop,
+             "frame_offset must be in [(n_fft - hop) / 2, n_fft / 2]");
+  ZV_REQUIRE(mag_eps >= 0.f && log_floor > 0.f, "bad mag_eps / log_floor");
+  f->off = frame_offset; f->mag_eps = mag_eps; f->log_floor = log_floor;
+  ZV_API_END
+}
+
 int zv_fbank_extract(zv_fbank_handle f, const float* wav, int64_t wav_ld, const int32_t* lens,
                      int B, int T_out, float* out, int64_t out_ld, void* stream) {
   ZV_API_BEGIN

@@ -80,6 +80,7 @@ SIGNATURES = {
     "zv_fbank_create": (_P, [_I, _I, _I, _P, _P]),
     "zv_fbank_destroy": (None, [_P]),
     "zv_fbank_extract": (_I, [_P, _P, ctypes.c_int64, _P, _I, _I, _P, ctypes.c_int64, _P]),
+    "zv_fbank_configure": (_I, [_P, _I, _F, _F]),
 }
 
 _lib = None

@@ -3,7 +3,7 @@
 batched form for serving.
 
 Steps, as the reference: prompt RMS normalisation to ``target_rms`` (:340-342)
--> VocosFbank prompt features (:345-347) -> ``(feat + feat_bias) * feat_scale``
+-> VocosFbank / BigVGANFbank prompt features (:345-347, :583-590) -> ``(feat + feat_bias) * feat_scale``
 (:349) -> ``model.sample(duration="predict")`` (:355-371) -> ``pred /
 feat_scale - feat_bias`` -> vocoder decode -> ``clamp(-1, 1)`` (:374-378) ->
 RTF metrics (:381-396) -> RMS restore (:399-400).  Text normalisation /
@@ -18,6 +18,17 @@ from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
 import torch
+
+
+def get_feature_extractor(feature_type: str, num_channels: int = 1):
+    """The reference's feature-extractor choice by ``model_config["feature"]["type"]``
+    (infer_zipvoice.py:583-590): "vocos" -> VocosFbank, "bigvgan_v2" -> BigVGANFbank."""
+    from .feature import BigVGANFbank, VocosFbank
+    if feature_type == "vocos":
+        return VocosFbank(num_channels=num_channels)
+    if feature_type == "bigvgan_v2":
+        return BigVGANFbank(num_channels=num_channels)
+    raise NotImplementedError(f"Unsupported feature type: {feature_type}")
 
 
 def _prompt_rms_normalise(wav: torch.Tensor, target_rms: float) -> Tuple[torch.Tensor, float]:
