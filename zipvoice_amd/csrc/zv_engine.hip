@@ -167,6 +167,10 @@ struct zv_engine {
   bool defer_stores = false;       // A/B: ZV_GEMM_DEFER=1 lets the next tile's K loop run past the
                                    // plain bf16 linears' stores (bitwise equal; up to 6 % in isolation,
                                    // ~1 % slower in the model: profiles/r01_gemm_defer_ab.txt)
+  bool pair_resid = false;         // A/B: ZV_PAIR_RESID=1 carries the bf16-mode residual stream as a
+                                   // bf16 hi/lo pair (8 B per update instead of 10): residual GEMMs
+                                   // -4..9 %, but the forward is unchanged (other kernels slower,
+                                   // profiles/r01_pair_resid_ab.txt); the fp32 stream stays default
   int fused_tile = 0;              // A/B: ZV_GEMM_FUSED_TILE 1 = GLU / NA in-projections on
                                    // 256-row 3-stage tiles (one 8-wave block per CU)
   int gemm_tile = 0;               // ZV_GEMM_TILE 0 (default): 128x128 two blocks per CU; A/B arms
@@ -196,6 +200,7 @@ struct zv_engine {
     sa_pos_mfma = envi("ZV_SA_POS_MFMA", 0) != 0;
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
+    pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
   }
   // ---------------------------------------------------------------- HIP graphs
   // The whole N-step Euler solve (~250 launches per step) is captured once per
@@ -507,6 +512,9 @@ struct zv_engine {
     const float* resid = nullptr;
     const float* rowvec = nullptr; long rowvec_ld = 0; int rows_per_group = 1;
     const float* orig = nullptr; const float* byp = nullptr;
+    // pair-residual form (bf16 mode): residual / bypass original as bf16 hi/lo pairs
+    const bf16* residh = nullptr; const bf16* residl = nullptr;
+    const bf16* origh = nullptr; const bf16* origl = nullptr;
   };
 
   static GemmParams gp_linear(const Linear& Lw, const Act& A, long M) {
@@ -526,6 +534,15 @@ struct zv_engine {
     p.Ch = o.act.h; p.Cl = o.act.l; p.ldch = o.act.ld;
     p.resid = o.resid; p.rowvec = o.rowvec; p.rowvec_ld = o.rowvec_ld;
     p.rows_per_group = o.rows_per_group; p.orig = o.orig; p.byp = o.byp;
+    p.residh = o.residh; p.residl = o.residl; p.origh = o.origh; p.origl = o.origl;
+    if constexpr (SPLIT == 1) {
+      if (o.residh) {   // pair-residual linear: own instantiation, the residual policy
+        if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 1>(p, 1, s, "gemm_bf16", true, gridx_resid);
+        else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 1>(p, 1, s, "gemm_bf16", true, gridx_resid);
+        return;
+      }
+    }
+    ZV_REQUIRE(!o.residh, "pair residual needs the bf16 mode");
     const char* tag = SPLIT == 3 ? "gemm_fp32" : "gemm_bf16";
     if (Lw.N <= 64) {   // own tag: the roofline's gemm_bf16 is the 128x128 instantiation alone
       launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD>(p, 1, s, SPLIT == 3 ? "gemm_fp32_n64" : "gemm_bf16_n64");
@@ -613,7 +630,12 @@ struct zv_engine {
       launch_attn_stats<SPLIT>(fp, s);
     }
     Out res;                       // cur = cur + module(cur), with the hi/lo copy
-    res.C = cur; res.ldc = D; res.resid = cur; res.act = cur_a;
+    const bool pairm = SPLIT == 1 && pair_resid;
+    if (pairm) {                   // the stream itself is the (hi, lo) pair
+      res.residh = cur_a.h; res.residl = cur_a.l; res.act = cur_a;
+    } else {
+      res.C = cur; res.ldc = D; res.resid = cur; res.act = cur_a;
+    }
     auto ff = [&](int f, const Out& oe) {
       Act hid = ws.hidden.get(M, W.ff_in[f].N, split);
       Out o1; o1.act = hid; o1.act_fn = 1;          // SwooshL fused (scaling.py:1322-1334)
@@ -703,19 +725,30 @@ struct zv_engine {
     self_attn(0);                                     // SA1 (+ temb)
     conv(0);                                          // conv1
     {                                                 // FF2 + bypass_mid (:593-598)
-      Out e = res; e.orig = src; e.byp = W.bypass_mid;
+      Out e = res; e.byp = W.bypass_mid;
+      if (pairm) { e.origh = src_a.h; e.origl = src_a.l; }
+      else e.orig = src;
       ff(1, e);
     }
     self_attn(1);                                     // SA2 (+ temb)
     conv(1);                                          // conv2
     {                                                 // FF3: only the fp32 stream feeds BiasNorm
-      Out e = res; e.act = Act{};                     // (which rewrites both copies): no bf16 copy
+      Out e = res;                                    // (which rewrites both copies): no bf16 copy
+      if (!pairm) e.act = Act{};
       ff(2, e);
     }
     // BiasNorm + bypass -> src; next layer's working copy (src + temb) -> cur
-    hipLaunchKernelGGL(zv_biasnorm_bypass_kernel, dim3(cdiv(M, 4)), dim3(256), 0, s, cur, src,
-                       W.norm_bias, W.norm_log_scale, W.bypass, src, src_a.h, src_a.l,
-                       has_next ? cur : nullptr, cur_a.h, cur_a.l, (long)D, temb, L, M, D);
+    if (pairm) {   // pair stream; fp32 output only for the stack's last layer (next stack's input)
+      ZV_REQUIRE(D % 8 == 0 && cur_a.ld == src_a.ld, "pair-residual BiasNorm layout");
+      hipLaunchKernelGGL(zv_biasnorm_bypass_pair_kernel, dim3(cdiv(M, 4)), dim3(256), 0, s, cur_a.h,
+                         cur_a.l, src_a.h, src_a.l, src_a.ld, W.norm_bias, W.norm_log_scale, W.bypass,
+                         has_next ? nullptr : src, src_a.h, src_a.l, has_next ? cur_a.h : nullptr,
+                         has_next ? cur_a.l : nullptr, temb, L, M, D);
+    } else {
+      hipLaunchKernelGGL(zv_biasnorm_bypass_kernel, dim3(cdiv(M, 4)), dim3(256), 0, s, cur, src,
+                         W.norm_bias, W.norm_log_scale, W.bypass, src, src_a.h, src_a.l,
+                         has_next ? cur : nullptr, cur_a.h, cur_a.l, (long)D, temb, L, M, D);
+    }
     ZV_LAUNCH_CHECK();
   }
 
@@ -725,8 +758,9 @@ struct zv_engine {
              int L, const uint8_t* pad, const float* temb, hipStream_t s) {
     const long M = (long)B * L;
     const bool split = SPLIT == 3;
-    float* cur = ws.cur.get<float>(M * Z.dim);
-    Act cur_a = ws.cur_a.get(M, Z.dim, split);
+    const bool pairm = SPLIT == 1 && pair_resid;
+    float* cur = pairm ? nullptr : ws.cur.get<float>(M * Z.dim);
+    Act cur_a = ws.cur_a.get(M, Z.dim, split || pairm);
     hipLaunchKernelGGL(zv_stack_entry_kernel, grid1d(M * Z.dim), dim3(256), 0, s, src, temb, cur,
                        src_a.h, src_a.l, cur_a.h, cur_a.l, (long)Z.dim, M, Z.dim, L);
     ZV_LAUNCH_CHECK();
@@ -745,7 +779,7 @@ struct zv_engine {
     const int D = Z.dim;
     const bool split = SPLIT == 3;
     float* main = ws.main.get<float>(M * D);
-    Act main_a = ws.main_a.get(M, D, split);
+    Act main_a = ws.main_a.get(M, D, split || (SPLIT == 1 && pair_resid));
     { Out o; o.C = main; o.ldc = D; linear<SPLIT>(Z.in_proj[sidx], xin, M, o, s); }
     // time embedding MLP (zipformer.py:267-278) + per-stack projections (:726-729)
     float* tstack = nullptr;
@@ -777,7 +811,7 @@ struct zv_engine {
       } else {
         const int dL = (T + S.ds - 1) / S.ds;
         float* d = ws.dsrc.get<float>((size_t)N * dL * D);
-        Act d_a = ws.dsrc_a.get((long)N * dL, D, split);
+        Act d_a = ws.dsrc_a.get((long)N * dL, D, split || (SPLIT == 1 && pair_resid));
         hipLaunchKernelGGL(zv_downsample_kernel, grid1d((long)N * dL * D), dim3(256), 0, s, main, d,
                            N, T, dL, D, S.ds, S.ds_w);
         ZV_LAUNCH_CHECK();
