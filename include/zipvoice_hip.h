@@ -185,6 +185,48 @@ int zv_vocoder_decode(zv_vocoder_handle v, const float* mel, int layout, float f
 int64_t zv_vocoder_device_bytes(zv_vocoder_handle v);
 
 /* ------------------------------------------------------------------------
+ * Vocoder (BigVGAN-v2, bigvgan_v2_24khz_100band_256x), the one the reference loads for
+ * feature.type "bigvgan_v2" (zipvoice/bin/infer_zipvoice.py:261-269: third-party
+ * bigvgan.BigVGAN.from_pretrained(..., use_cuda_kernel=False) + remove_weight_norm();
+ * decode(mel) = forward(mel)).  Weights are the weight-norm-removed state dict.
+ * ---------------------------------------------------------------------- */
+typedef struct zv_bigvgan* zv_bigvgan_handle;
+
+/* Mirrors the bigvgan config.json fields the generator reads. */
+typedef struct {
+  int precision;                    /* zv_precision (ZV_FP32 = split-bf16x3 GEMMs) */
+  int num_mels;                     /* 100 */
+  int upsample_initial_channel;     /* 1536 */
+  int num_upsamples;                /* len(upsample_rates) (6), <= 8 */
+  int upsample_rates[8];            /* 4 4 2 2 2 2 */
+  int upsample_kernel_sizes[8];     /* 8 8 4 4 4 4 */
+  int num_kernels;                  /* len(resblock_kernel_sizes) (3), <= 3 */
+  int resblock_kernel_sizes[3];     /* 3 7 11 */
+  int resblock_dilation_sizes[3][3];/* (1 3 5) x 3; resblock "1" (AMPBlock1) */
+  int snake_logscale;               /* 1 */
+  int use_tanh_at_final;            /* 0: clamp(-1, 1) */
+  int use_bias_at_final;            /* 0 */
+} zv_bigvgan_config;
+
+zv_bigvgan_handle zv_bigvgan_create(const zv_bigvgan_config* cfg);
+void zv_bigvgan_destroy(zv_bigvgan_handle v);
+/* Stage one generator tensor ("conv_pre.weight", "ups.0.0.weight",
+ * "resblocks.4.convs1.2.bias", "resblocks.4.activations.3.act.alpha",
+ * "activation_post.act.beta", "conv_post.weight", ...); the alias-free filter buffers
+ * (*.upsample.filter, *.downsample.lowpass.filter) are accepted and checked. */
+int zv_bigvgan_set_weight(zv_bigvgan_handle v, const char* name, const float* host_data,
+                          int64_t numel);
+int zv_bigvgan_finalize(zv_bigvgan_handle v);
+/* wav[b, :T*hop] = forward(mel_b), hop = prod(upsample_rates); arguments as
+ * zv_vocoder_decode (layout 0 [B, num_mels, T] / 1 [B, T, num_mels] with
+ * x / feat_scale - feat_bias; lens [B] device frame counts or NULL).  The final
+ * clamp (or tanh) is part of the network. */
+int zv_bigvgan_decode(zv_bigvgan_handle v, const float* mel, int layout, float feat_scale,
+                      float feat_bias, const int32_t* lens, int B, int T, float* wav,
+                      void* stream);
+int64_t zv_bigvgan_device_bytes(zv_bigvgan_handle v);
+
+/* ------------------------------------------------------------------------
  * Prompt feature extractor (VocosFbank: centred reflect-padded STFT, power 1,
  * mel projection, log(clamp(1e-7)); fp32 arithmetic throughout).
  * ---------------------------------------------------------------------- */

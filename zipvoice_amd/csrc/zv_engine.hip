@@ -999,6 +999,7 @@ struct zv_engine {
 };
 
 #include "zv_vocoder.inc"
+#include "zv_bigvgan.inc"
 #include "zv_fbank.inc"
 
 // ===========================================================================
@@ -1400,6 +1401,55 @@ int zv_vocoder_decode(zv_vocoder_handle v, const float* mel, int layout, float f
     v->decode<1>(mel, layout, feat_scale, feat_bias, lens, B, T, wav, clamp, s);
   ZV_API_END
 }
+
+// ---------------------------------------------------------------- BigVGAN
+zv_bigvgan_handle zv_bigvgan_create(const zv_bigvgan_config* cfg) {
+  try {
+    ZV_REQUIRE(cfg != nullptr, "null bigvgan config");
+    ZV_REQUIRE(cfg->precision == ZV_FP32 || cfg->precision == ZV_BF16, "bad precision");
+    ZV_REQUIRE(cfg->num_mels > 0 && cfg->upsample_initial_channel > 0, "bad bigvgan dimensions");
+    return new zv_bigvgan(*cfg);
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return nullptr;
+  }
+}
+
+void zv_bigvgan_destroy(zv_bigvgan_handle v) { delete v; }
+
+int zv_bigvgan_set_weight(zv_bigvgan_handle v, const char* name, const float* host_data,
+                          int64_t numel) {
+  ZV_API_BEGIN
+  ZV_REQUIRE(v && name && (host_data || numel == 0), "bad arguments");
+  ZV_REQUIRE(!v->ready, "bigvgan already finalized");
+  v->staged[name].assign(host_data, host_data + numel);
+  ZV_API_END
+}
+
+int zv_bigvgan_finalize(zv_bigvgan_handle v) {
+  ZV_API_BEGIN
+  ZV_REQUIRE(v != nullptr, "null bigvgan handle");
+  v->finalize();
+  ZV_API_END
+}
+
+int zv_bigvgan_decode(zv_bigvgan_handle v, const float* mel, int layout, float feat_scale,
+                      float feat_bias, const int32_t* lens, int B, int T, float* wav,
+                      void* stream) {
+  ZV_API_BEGIN
+  ZV_REQUIRE(v != nullptr && v->ready, "bigvgan not finalized (call zv_bigvgan_finalize)");
+  ZV_REQUIRE(B > 0 && T > 0, "empty batch");
+  ZV_REQUIRE(layout == 0 || layout == 1, "layout must be 0 (B,C,T) or 1 (B,T,C)");
+  ZV_REQUIRE(feat_scale != 0.f, "feat_scale must be nonzero");
+  hipStream_t s = (hipStream_t)stream;
+  if (v->cfg.precision == ZV_FP32)
+    v->decode<3>(mel, layout, feat_scale, feat_bias, lens, B, T, wav, s);
+  else
+    v->decode<1>(mel, layout, feat_scale, feat_bias, lens, B, T, wav, s);
+  ZV_API_END
+}
+
+int64_t zv_bigvgan_device_bytes(zv_bigvgan_handle v) { return v ? (int64_t)v->device_bytes() : 0; }
 
 zv_fbank_handle zv_fbank_create(int n_fft, int hop, int n_mels, const float* host_window,
                                 const float* host_fb) {

@@ -76,6 +76,12 @@ SIGNATURES = {
     "zv_vocoder_finalize": (_I, [_P]),
     "zv_vocoder_decode": (_I, [_P, _P, _I, _F, _F, _P, _I, _I, _P, _I, _P]),
     "zv_vocoder_device_bytes": (ctypes.c_int64, [_P]),
+    "zv_bigvgan_create": (_P, [_P]),
+    "zv_bigvgan_destroy": (None, [_P]),
+    "zv_bigvgan_set_weight": (_I, [_P, ctypes.c_char_p, _P, ctypes.c_int64]),
+    "zv_bigvgan_finalize": (_I, [_P]),
+    "zv_bigvgan_decode": (_I, [_P, _P, _I, _F, _F, _P, _I, _I, _P, _P]),
+    "zv_bigvgan_device_bytes": (ctypes.c_int64, [_P]),
     # prompt feature extractor (zipvoice_amd/feature.py)
     "zv_fbank_create": (_P, [_I, _I, _I, _P, _P]),
     "zv_fbank_destroy": (None, [_P]),

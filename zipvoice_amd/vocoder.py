@@ -306,7 +306,8 @@ class Vocos:
 
 def get_vocoder(vocos_local_path: Optional[str] = None, type: str = "vocos",
                 precision: str = "fp32"):
-    """Mirror of infer_zipvoice.py:249-273."""
+    """Mirror of infer_zipvoice.py:249-273 ("vocos" / "bigvgan_v2"; a local directory
+    stands in for the Hub id)."""
     if type == "vocos":
         if vocos_local_path:
             voc = Vocos.from_hparams(f"{vocos_local_path}/config.yaml", precision=precision)
@@ -315,4 +316,8 @@ def get_vocoder(vocos_local_path: Optional[str] = None, type: str = "vocos",
             voc.load_state_dict(blob)
             return voc
         return Vocos.from_pretrained("charactr/vocos-mel-24khz", precision=precision)
+    if type == "bigvgan_v2":                       # infer_zipvoice.py:261-269
+        from .bigvgan import BigVGAN
+        return BigVGAN.from_pretrained(vocos_local_path or "nvidia/bigvgan_v2_24khz_100band_256x",
+                                       use_cuda_kernel=False, precision=precision)
     raise NotImplementedError(f"Unsupported vocoder type: {type}")
