@@ -50,3 +50,19 @@ def test_generate_batch_ragged(stack):
     assert len(outs) == 2 and met["rtf"] > 0
     for o in outs:
         assert o.dim() == 2 and o.shape[1] > 0 and torch.isfinite(o).all()
+
+
+def test_generate_sentence_bigvgan_stack(stack):
+    """feature.type "bigvgan_v2" (egs/zipvoice/conf/zipvoice_base_bigvgan_v2.json):
+    BigVGANFbank prompt features + the BigVGAN-v2 vocoder, through the same flow."""
+    from zipvoice_amd.bigvgan import BigVGAN
+    from zipvoice_amd.infer import get_feature_extractor
+    m, _, _ = stack
+    voc = BigVGAN(precision="bf16").load_synthetic(0).to("cuda:0")
+    fx = get_feature_extractor("bigvgan_v2")
+    wav, met = generate_sentence(list(range(1, 30)), list(range(40, 52)), prompt(24000, 3), m,
+                                 voc, fx, num_step=4)
+    assert wav.shape[0] == 1 and wav.shape[1] % 256 == 0 and wav.shape[1] > 0
+    assert torch.isfinite(wav).all()
+    assert float(wav.abs().max()) <= 1.0 * 0.05 / 0.1 + 1e-6
+    assert met["rtf_vocoder"] > 0
