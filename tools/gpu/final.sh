@@ -6,7 +6,7 @@ set -o pipefail
 OUT=gpurun_out/final
 mkdir -p $OUT
 export TMPDIR=/tmp
-RX='zv_gemm_kernel<128, 128, 2, 2, 1, 0, 2, 2, 64>'
+RX='zv_gemm_kernel<128, 128, 2, 2, 1, 0, 2, 2, 64, 0, 0, 0>'
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && \
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv --kernel-include-regex zv_gemm_kernel -d $OUT/pmc_fetch -o run -- python3 tools/profile_forward.py --iters 1 > $OUT/pmc_fetch.log 2>&1 && \

@@ -1183,6 +1183,8 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
     case 30: ms = bench_variant<128, 128, 2, 2, 4, 32>(p, iters, persistent, s); break;
     case 40: ms = bench_variant<128, 128, 2, 2, 2, GEMM_BK, 8>(p, iters, persistent, s); break;
     case 31: ms = bench_variant<128, 128, 2, 2, 3, 32>(p, iters, persistent, s); break;
+    case 32: ms = bench_variant<256, 128, 2, 2, 2, 32>(p, iters, persistent, s); break;
+    case 33: ms = bench_variant<256, 128, 2, 2, 3, 32>(p, iters, persistent, s); break;
     case 20: ms = bench_variant8<0, true>(p, iters, s); break;
     case 21: ms = bench_variant8<1, true>(p, iters, s); break;
     case 22: ms = bench_variant8<0, false>(p, iters, s); break;
