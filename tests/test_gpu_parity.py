@@ -181,3 +181,33 @@ def test_dialog_long_sequence_fused_vs_materialized():
     f = fused.float().cpu().numpy()[valid]
     r = ref.float().cpu().numpy()[valid]
     check(f, r, "bf16", f"dialog T={T} bf16 fused vs fp32 materialised")
+
+
+@pytest.mark.parametrize("T,lens", [(1, [1]), (2, [2, 1]), (5, [5, 3]), (9, [9, 1])])
+def test_velocity_tiny_lengths(T, lens):
+    """Edge lengths below the stacks' downsampling factors (1..4): single frames, a
+    one-frame item padded inside a longer batch, odd lengths, against the oracle."""
+    from oracle.zipvoice_np import ZipVoiceOracle
+    from zipvoice_amd.weights import synthetic_state_dict
+    m = model("zipvoice", "fp32")
+    o = ZipVoiceOracle(m.cfg, synthetic_state_dict(m.cfg, 0))
+    rng = np.random.default_rng(T)
+    B = len(lens)
+    x = rng.standard_normal((B, T, 100), dtype=np.float32)
+    tc = rng.standard_normal((B, T, 100), dtype=np.float32)
+    sc = rng.standard_normal((B, T, 100), dtype=np.float32)
+    pm = np.arange(T)[None] >= np.array(lens)[:, None]
+    v = m.engine.velocity(0.6, 1.0, cuda(x), cuda(tc), cuda(sc), cuda(pm))
+    ref = o.velocity(np.float32(0.6), x, tc, sc, pm, 1.0)
+    check(v, ref, "fp32", f"velocity T={T} lens={lens}")
+
+
+def test_empty_batch_rejected():
+    """B = 0 / T = 0 are refused by the C ABI with an error (no launch)."""
+    m = model("zipvoice", "fp32")
+    z = torch.zeros(0, 4, 100, device="cuda:0")
+    with pytest.raises(RuntimeError):
+        m.engine.velocity(0.5, 1.0, z, z, z, torch.zeros(0, 4, dtype=torch.bool, device="cuda:0"))
+    z = torch.zeros(1, 0, 100, device="cuda:0")
+    with pytest.raises(RuntimeError):
+        m.engine.velocity(0.5, 1.0, z, z, z, torch.zeros(1, 0, dtype=torch.bool, device="cuda:0"))
