@@ -577,10 +577,14 @@ struct zv_engine {
         return;
       }
     }
-    const bool occ2 = o.resid ? occ_resid == 2 : occ_plain == 2;
-    const int gx = o.resid ? gridx_resid : gridx_plain;
-    if (occ2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2>(p, 1, s, tag, true, gx);
-    else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1>(p, 1, s, tag, true, gx);
+    if (o.resid) {   // residual-stream linear: its own symbol / tag (HBM roofline)
+      const char* rtag = SPLIT == 3 ? "gemm_fp32_resid" : "gemm_bf16_resid";
+      if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 1>(p, 1, s, rtag, true, gridx_resid);
+      else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 1>(p, 1, s, rtag, true, gridx_resid);
+      return;
+    }
+    if (occ_plain == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2>(p, 1, s, tag, true, gridx_plain);
+    else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1>(p, 1, s, tag, true, gridx_plain);
   }
 
   // ---------------------------------------------------------------- one layer
