@@ -18,6 +18,7 @@
 
 #include "zv_common.h"
 #include "zv_gemm.inc"
+#include "zv_gemm_ws.inc"
 #include "zv_gemm8.inc"
 #include "zv_attn.inc"
 #include "zv_elem.inc"
@@ -159,6 +160,8 @@ struct zv_engine {
   // one tile per block (gridx -1), the others persistent over the resident grid (0).
   int occ_plain = 2, occ_resid = 2, occ_fused = 2;
   int gridx_plain = 0, gridx_resid = -1, gridx_fused = 0;
+  int resid_ws = 1;                // residual linears on the wave-specialised epilogue kernel:
+                                   // ZV_RESID_WS 1 = K <= 64 only (default), 2 = all, 0 = none
   bool sa_pos_mfma = false;        // A/B: ZV_SA_POS_MFMA=1 puts the SelfAttention positional term on
                                    // f32 MFMA (parity-green, same time: the loop is latency bound)
   bool skinny_tiles = true;        // V^T projection (N = 48) on 64x64 tiles, one per block
@@ -201,6 +204,7 @@ struct zv_engine {
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
+    resid_ws = envi("ZV_RESID_WS", 1);
   }
   // ---------------------------------------------------------------- HIP graphs
   // The whole N-step Euler solve (~250 launches per step) is captured once per
@@ -579,6 +583,15 @@ struct zv_engine {
     }
     if (o.resid) {   // residual-stream linear: its own symbol / tag (HBM roofline)
       const char* rtag = SPLIT == 3 ? "gemm_fp32_resid" : "gemm_bf16_resid";
+      if constexpr (SPLIT == 1)
+        // wave-specialised epilogue (zv_gemm_ws.inc): faster where the linear is all epilogue
+        // (K <= 64: SelfAttention out-projections, -8 %); its single 4-wave MMA group per CU
+        // loses to zv_gemm_kernel's two co-resident blocks on longer K loops (+40 % at K = 1536,
+        // profiles/r01_resid_ws_ab.txt)
+        if (Lw.N % 128 == 0 && !o.act.l && (resid_ws == 2 || (resid_ws == 1 && Lw.K <= 64))) {
+          launch_gemm_resid_ws(p, s, "gemm_bf16_resid_ws");   // own tag: one symbol per roofline tag
+          return;
+        }
       if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 1>(p, 1, s, rtag, true, gridx_resid);
       else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 1>(p, 1, s, rtag, true, gridx_resid);
       return;
