@@ -1,20 +1,27 @@
 #!/usr/bin/env python3
 """Benchmark: generated mel-frames/s (whole job) + RTF of ZipVoice sampling.
 
-Workload (BASELINE.json configs[1], "C2"): ZipVoice 123M (synthetic seeded
-weights — no pretrained weights offline), bf16 MFMA, N_steps=16, batch of 32
-utterances per GPU, each a 3 s prompt (281 frames, 40 prompt tokens) + 10 s of
-generated speech (938 frames, 134 text tokens; duration="real"), so T = 1219
-frames, classifier-free guidance 1.0 (batch doubled to 64 inside the engine),
-t_shift 0.5.  One "step" = what the reference's RTF times
-(``infer_zipvoice.py:359-386``): one full ``ZipVoice.sample()`` of the batch
-(text encoder, conditions, the 16-step guided Euler loop) followed by the
-vocoder on the generated features (post-processing + Vocos decode + clamp,
-``:374-378``; synthetic vocos-mel-24khz weights, fp32-accurate mode), plus, for
-N > 1 GPUs, the RCCL all-gather that reassembles the output wav batch on every
-rank.
+Workloads (BASELINE.json configs), synthetic seeded weights (no
+pretrained weights offline) and synthetic inputs of the configs' shapes:
 
-Launch: python bench.py [--gpus N --steps K --warmup W]
+* C2 (default; the metric's configuration, BASELINE configs[1]): ZipVoice 123M,
+  bf16 MFMA, N_steps=16, 32 utterances per GPU, each a 3 s prompt (281 frames, 40
+  prompt tokens) + 10 s of generated speech (938 frames, 134 text tokens;
+  duration="real"), T = 1219 frames, classifier-free guidance 1.0 (64 decoder rows
+  per GPU), t_shift 0.5.  Weak scaling: the global batch is 32 x N utterances.
+* C3 (``--config C3``, BASELINE configs[2]): ZipVoice-Distill, N_steps=8, guidance
+  3.0 through the guidance embedding (no CFG doubling), a fixed global batch of 128
+  utterances of the same shape sharded over the N GPUs (strong scaling).
+
+One "step" = what the reference's RTF times (``infer_zipvoice.py:359-386``) for the
+whole global batch, run data-parallel (``zipvoice_amd.dist.generate_batch_dp``):
+every rank takes its contiguous shard of the global batch, runs ``ZipVoice.sample()``
+(text encoder, conditions, the guided Euler loop replayed as one HIP graph) and the
+vocoder on the generated features (post-processing + Vocos decode + clamp, ``:374-378``),
+and one RCCL all-gather over xGMI reassembles the output wav batch on every rank.
+Inputs are resident in HBM before the timed region.
+
+Launch: python bench.py [--gpus N --steps K --warmup W --config C2|C3]
         (N > 1 under torch.distributed.run, one process per GPU).
 """
 import argparse
@@ -29,44 +36,70 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-# C2 shapes
-B_PER_GPU = 32
+# per-utterance shape of C2/C3
 T_PROMPT = 281
 S_PROMPT = 40
 S_TEXT = 134
 T_GEN = 938
-NUM_STEP = 16
-GUIDANCE = 1.0
 T_SHIFT = 0.5
 SAMPLE_RATE = 24000
 HOP = 256
+CONFIGS = {
+    "C2": dict(variant="zipvoice", num_step=16, guidance=1.0, per_gpu=32, global_batch=None,
+               scaling="weak", cfg_rows=2,
+               desc="C2: ZipVoice 123M, N_steps=16, batch=32/GPU x (3 s prompt + 10 s generated; "
+                    "T=1219 frames), CFG g=1.0 (64 decoder rows per GPU), t_shift=0.5"),
+    "C3": dict(variant="zipvoice_distill", num_step=8, guidance=3.0, per_gpu=None,
+               global_batch=128, scaling="strong", cfg_rows=1,
+               desc="C3: ZipVoice-Distill 123M, N_steps=8, global batch=128 x (3 s prompt + 10 s "
+                    "generated; T=1219 frames) sharded over the GPUs, guidance 3.0 (embedding, "
+                    "no CFG doubling), t_shift=0.5"),
+}
 BF16_DENSE_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16
 FP32_MFMA_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
-# PMC traffic per launch (tools/pmc_traffic.py, tools/gpu/final.sh) of the two GEMM instantiations
-# the roofline reports: the residual-stream linears (ROLE = 1) and the plain / activation linears
-TRAFFIC_FILES = {"gemm_bf16_resid": "r01_gemm_resid_traffic.json", "gemm_bf16": "r01_gemm_traffic.json"}
+# PMC traffic per launch (tools/pmc_traffic.py) of the two GEMM families the roofline
+# reports: the residual-stream linears (ROLE = 1) and the plain / activation linears
+# (newest measurement first)
+TRAFFIC_FILES = {"gemm_bf16_resid": ["r02_gemm_resid_traffic.json", "r01_gemm_resid_traffic.json"],
+                 "gemm_bf16": ["r02_gemm_traffic.json", "r01_gemm_traffic.json"]}
+# analytic FLOPs of one decoder sequence-forward (FlopCounterMode fit on the
+# reference, within 1 %) and of the vocoder per frame
+def decoder_flops(T):
+    return 146.3e6 * T + 9920.0 * T * T
 
 
-def make_inputs(rank, device):
-    rng = np.random.default_rng(1000 + rank)
-    tokens = [[int(v) for v in rng.integers(1, 360, S_TEXT)] for _ in range(B_PER_GPU)]
-    ptokens = [[int(v) for v in rng.integers(1, 360, S_PROMPT)] for _ in range(B_PER_GPU)]
-    pf = (0.3 * rng.standard_normal((B_PER_GPU, T_PROMPT, 100)) - 0.5).astype(np.float32)
-    plens = np.full(B_PER_GPU, T_PROMPT, np.int64)
-    flens = np.full(B_PER_GPU, T_GEN, np.int64)
-    T = T_PROMPT + T_GEN
-    x0 = np.random.default_rng(666 + rank).standard_normal((B_PER_GPU, T, 100), dtype=np.float32)
-    to = lambda a: torch.from_numpy(a).to(device)  # noqa: E731
-    return dict(tokens=tokens, prompt_tokens=ptokens, prompt_features=to(pf),
-                prompt_features_lens=to(plens), features_lens=to(flens), x0=to(x0))
+VOCODER_FLOPS_PER_FRAME = 27e6
 
 
-def build(precision, device):
+def item_arrays(i):
+    """Utterance i of the synthetic global batch (the same on every rank)."""
+    rng = np.random.default_rng([1000, i])
+    tokens = [int(v) for v in rng.integers(1, 360, S_TEXT)]
+    ptokens = [int(v) for v in rng.integers(1, 360, S_PROMPT)]
+    pf = (0.3 * rng.standard_normal((T_PROMPT, 100)) - 0.5).astype(np.float32)
+    x0 = np.random.default_rng([666, i]).standard_normal((T_PROMPT + T_GEN, 100),
+                                                         dtype=np.float32)
+    return tokens, ptokens, pf, x0
+
+
+def materialize(ids, device):
+    """Device-resident inputs of a shard (built before the timed region)."""
+    arrs = [item_arrays(i) for i in ids]
+    b = len(ids)
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+    return dict(tokens=[a[0] for a in arrs], prompt_tokens=[a[1] for a in arrs],
+                prompt_features=to(np.stack([a[2] for a in arrs])) if b else None,
+                prompt_features_lens=to(np.full(b, T_PROMPT, np.int64)),
+                features_lens=to(np.full(b, T_GEN, np.int64)),
+                x0=to(np.stack([a[3] for a in arrs])) if b else None)
+
+
+def build(variant, precision, device):
     from zipvoice_amd.config import default_config
     from zipvoice_amd.models import build_model
     from zipvoice_amd.weights import synthetic_state_dict
-    cfg = default_config("zipvoice")
+    cfg = default_config(variant)
     m = build_model(cfg, precision=precision)
     m.load_state_dict(synthetic_state_dict(cfg, 0))
     return m.to(device)
@@ -77,31 +110,50 @@ def build_vocoder(device):
     return Vocos(precision="fp32").load_synthetic(0).to(device)
 
 
-def run_step(model, vocoder, inp, world, rank):
-    gen, gen_lens, _, _ = model.sample(
-        tokens=inp["tokens"], prompt_tokens=inp["prompt_tokens"],
-        prompt_features=inp["prompt_features"], prompt_features_lens=inp["prompt_features_lens"],
-        features_lens=inp["features_lens"], t_shift=T_SHIFT, duration="real",
-        num_step=NUM_STEP, guidance_scale=GUIDANCE, x0=inp["x0"])
-    wav = vocoder.decode_features(gen, gen_lens, feat_scale=0.1, feat_bias=0.0, clamp=True)
-    if world > 1:
-        # the one exchange of the data-parallel path: reassemble the output wav
-        # batch on every rank (RCCL all-gather over xGMI), zipvoice_amd/dist.py
-        from zipvoice_amd.dist import all_gather_padded
-        wav, _ = all_gather_padded(wav.unsqueeze(-1), gen_lens * HOP)
-    return wav
+class Job:
+    """One benchmark step: generate_batch_dp over the global batch."""
+
+    def __init__(self, conf, model, vocoder, n_items, device):
+        from zipvoice_amd.dist import shard_bounds, _world_rank
+        self.conf, self.model, self.vocoder, self.device = conf, model, vocoder, device
+        self.items = list(range(n_items))
+        self.costs = [T_PROMPT + T_GEN] * n_items      # frames per utterance
+        world, rank = _world_rank()
+        lo, hi = shard_bounds(self.costs, world)[rank]
+        self.inp = materialize(self.items[lo:hi], device)
+        self.n_local = hi - lo
+
+    def compute(self, shard):
+        assert len(shard) == self.n_local
+        if not shard:
+            return (torch.zeros((0, 1), device=self.device),
+                    torch.zeros((0,), dtype=torch.int64, device=self.device))
+        inp = self.inp
+        gen, gen_lens, _, _ = self.model.sample(
+            tokens=inp["tokens"], prompt_tokens=inp["prompt_tokens"],
+            prompt_features=inp["prompt_features"],
+            prompt_features_lens=inp["prompt_features_lens"],
+            features_lens=inp["features_lens"], t_shift=T_SHIFT, duration="real",
+            num_step=self.conf["num_step"], guidance_scale=self.conf["guidance"], x0=inp["x0"])
+        wav = self.vocoder.decode_features(gen, gen_lens, feat_scale=0.1, feat_bias=0.0,
+                                           clamp=True)
+        return wav, gen_lens * HOP
+
+    def step(self):
+        from zipvoice_amd.dist import generate_batch_dp
+        return generate_batch_dp(self.items, self.compute, self.costs)
 
 
-def timed(model, vocoder, inp, steps, warmup, world, rank):
+def timed(job, steps, warmup, world):
     import torch.distributed as dist
     for _ in range(warmup):
-        run_step(model, vocoder, inp, world, rank)
+        job.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
-        run_step(model, vocoder, inp, world, rank)
+        job.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -127,9 +179,10 @@ def _kernel_roofline(name, r, total_ms):
         peak = BF16_DENSE_PEAK_TFLOPS if "bf16" in name else FP32_MFMA_PEAK_TFLOPS
         unit = "TFLOP/s"
     traffic, tsrc = None, None
-    tfile = TRAFFIC_FILES.get(name)
+    tfile = next((f for f in TRAFFIC_FILES.get(name, [])
+                  if os.path.exists(os.path.join(REPO, "profiles", f))), None)
     tpath = os.path.join(REPO, "profiles", tfile) if tfile else None
-    if tpath and os.path.exists(tpath):
+    if tpath:
         with open(tpath) as f:
             t = json.load(f)
         traffic = t.get("traffic_bytes_per_launch")
@@ -149,14 +202,14 @@ def _kernel_roofline(name, r, total_ms):
     return out
 
 
-def roofline(model, vocoder, inp):
+def roofline(job):
     """One extra, untimed step with the engine's per-launch HIP-event profiler on:
     the dominant kernel's algorithmic work per launch / its average duration (HIP events
     on the launch stream), plus the same object for the plain GEMM family."""
     from zipvoice_amd import engine
     torch.cuda.synchronize()
     engine.profile(True)
-    run_step(model, vocoder, inp, 1, 0)
+    job.compute(list(range(job.n_local)))
     torch.cuda.synchronize()
     rep = engine.profile_report()
     engine.profile(False)
@@ -169,17 +222,17 @@ def roofline(model, vocoder, inp):
     return res
 
 
-def cpu_baseline(budget_s=12.0):
+def cpu_baseline(variant, guidance, num_step, budget_s=12.0):
     """Oracle (numpy fp32 restatement, oracle/zipvoice_np.py) on the host cores: one
-    utterance of the same workload (CFG batch of 2, T=1219), guided velocity
-    evaluations repeated until ~budget_s, scaled to generated frames/s."""
+    utterance of the same workload (T=1219; CFG batch of 2 where the model guides),
+    velocity evaluations repeated until ~budget_s, scaled to generated frames/s."""
     from threadpoolctl import threadpool_limits
 
     from oracle.zipvoice_np import ZipVoiceOracle
     from zipvoice_amd.config import default_config
     from zipvoice_amd.weights import synthetic_state_dict
     cores = min(16, len(os.sched_getaffinity(0)))
-    cfg = default_config("zipvoice")
+    cfg = default_config(variant)
     o = ZipVoiceOracle(cfg, synthetic_state_dict(cfg, 0))
     rng = np.random.default_rng(7)
     T = T_PROMPT + T_GEN
@@ -191,27 +244,30 @@ def cpu_baseline(budget_s=12.0):
     with threadpool_limits(limits=cores):
         t0 = time.perf_counter()
         while True:
-            o.velocity(np.float32(0.3), x, tc, sc, pm, GUIDANCE)
+            o.velocity(np.float32(0.3), x, tc, sc, pm, guidance)
             n += 1
             if time.perf_counter() - t0 > budget_s or n >= 8:
                 break
         dt = (time.perf_counter() - t0) / n
-    frames_per_s = T_GEN / (NUM_STEP * dt)
+    frames_per_s = T_GEN / (num_step * dt)
     return {"value": round(frames_per_s, 2), "unit": "mel-frames/s", "cores": cores,
             "kind": "port",
-            "sample": f"{n} guided velocity evaluations (CFG batch 2 x T={T}) of one utterance; "
-                      f"{dt:.2f} s each; frames/s = {T_GEN} / (16 steps x time per evaluation)"}
+            "sample": f"{n} velocity evaluations (T={T}, {variant}, g={guidance}) of one "
+                      f"utterance; {dt:.2f} s each; frames/s = {T_GEN} / ({num_step} steps x time "
+                      f"per evaluation); vocoder excluded"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fp32-mode", action="store_true")
     args = ap.parse_args()
+    conf = CONFIGS[args.config]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -222,40 +278,56 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=device)
 
-    model = build(args.precision, device)
+    n_items = conf["global_batch"] or conf["per_gpu"] * world
+    model = build(conf["variant"], args.precision, device)
     vocoder = build_vocoder(device)
-    inp = make_inputs(rank, device)
-    ms = timed(model, vocoder, inp, args.steps, args.warmup, world, rank) * 1e3
-    frames = B_PER_GPU * T_GEN * world
+    job = Job(conf, model, vocoder, n_items, device)
+    ms = timed(job, args.steps, args.warmup, world) * 1e3
+    frames = n_items * T_GEN
     value = frames / (ms * 1e-3)
-    audio_s_per_gpu = B_PER_GPU * T_GEN * HOP / SAMPLE_RATE
-    rtf = (ms * 1e-3) / audio_s_per_gpu
+    audio_s = n_items * T_GEN * HOP / SAMPLE_RATE
+    rtf = (ms * 1e-3) / audio_s                      # whole job
+    T = T_PROMPT + T_GEN
+    path_flops = (n_items * conf["cfg_rows"] * conf["num_step"] * decoder_flops(T)
+                  + n_items * T_GEN * VOCODER_FLOPS_PER_FRAME)
+    path_tfs = path_flops / (ms * 1e-3) / 1e12
     result = {
-        "metric": "generated mel-frames/s (whole job) + RTF, ZipVoice 123M N_steps=16 batch=32/GPU",
+        "metric": "generated mel-frames/s (whole job) + RTF, ZipVoice 123M N_steps=16 batch=32/GPU"
+                  if args.config == "C2" else
+                  "generated mel-frames/s (whole job) + RTF, ZipVoice-Distill N_steps=8 batch=128",
         "value": round(value, 1), "unit": "mel-frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
-        "rtf_per_gpu": round(rtf, 6), "x_realtime_per_gpu": round(1.0 / rtf, 1),
-        "config": {"workload": "C2: ZipVoice 123M, N_steps=16, batch=32x(3 s prompt + 10 s "
-                               "generated; T=1219 frames), CFG g=1.0 (64 rows), t_shift=0.5",
-                   "model": "ZipVoice-123M (zipvoice_base.json, synthetic seeded weights)",
-                   "global_batch": B_PER_GPU * world, "seq_len": T_PROMPT + T_GEN,
-                   "parallelism": f"dp{world}"},
+        "scaling": conf["scaling"], "vs_baseline": None, "dtype": args.precision,
+        "data": "synthetic (seeded weights and inputs of the config's shapes)",
+        "rtf": round(rtf, 6), "x_realtime_per_gpu": round(1.0 / (rtf * world), 1),
+        "config": {"workload": conf["desc"],
+                   "model": f"{conf['variant']} (zipvoice_base.json, synthetic seeded weights)",
+                   "global_batch": n_items, "seq_len": T, "parallelism": f"dp{world}"},
+        # the path is a dense contraction priced on the bf16 MFMA peak
+        "path_roofline": {"algorithmic_tflop_per_step": round(path_flops / 1e12, 2),
+                          "achieved_tflops": round(path_tfs, 1),
+                          "peak_tflops": BF16_DENSE_PEAK_TFLOPS * world,
+                          "frac": round(path_tfs / (BF16_DENSE_PEAK_TFLOPS * world), 4),
+                          "flops_source": "F(T)=146.3e6*T+9920*T^2 per decoder sequence-forward "
+                                          "(SURVEY.md §6) x rows x steps + 27 MFLOP/frame vocoder"},
     }
     if rank == 0:
-        result["roofline"] = roofline(model, vocoder, inp)
+        result["roofline"] = roofline(job)
         if world == 1 and not args.no_fp32_mode and args.precision == "bf16":
-            del model
+            del job, model
             torch.cuda.empty_cache()
-            m32 = build("fp32", device)
-            ms32 = timed(m32, vocoder, inp, 1, 1, 1, 0) * 1e3
+            m32 = build(conf["variant"], "fp32", device)
+            job32 = Job(conf, m32, vocoder, n_items, device)
+            ms32 = timed(job32, 1, 2, 1) * 1e3        # after two warm-ups (graph captured)
             result["fp32_accurate_mode"] = {
                 "ms_per_step": round(ms32, 2),
-                "value": round(B_PER_GPU * T_GEN / (ms32 * 1e-3), 1), "unit": "mel-frames/s",
-                "note": "bf16x3 split-product GEMMs; the parity mode (mean |err| ~3e-5 vs reference)"}
-            del m32
+                "value": round(frames / (ms32 * 1e-3), 1), "unit": "mel-frames/s",
+                "note": "bf16x3 split-product GEMMs; the parity mode (mean |err| ~3e-5 vs reference); "
+                        "timed after 2 warm-up steps"}
+            del job32, m32
         if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline()
+            result["cpu_baseline"] = cpu_baseline(conf["variant"], conf["guidance"],
+                                                  conf["num_step"])
         print(json.dumps(result), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -84,8 +84,10 @@ int zv_set_weight(zv_handle h, const char* name, const float* host_data, int64_t
 /* Check that every tensor of the config's state dict was staged (strict=True),
  * convert/pad to the device layout and upload.  Synchronous. */
 int zv_finalize(zv_handle h);
-/* Pre-size the workspace for batches up to max_batch rows of max_frames frames
- * (optional; forward calls grow it on demand, which synchronises). */
+/* Pre-size the decoder workspace for guided calls of up to max_batch utterances of
+ * max_frames frames (runs one uncaptured guided velocity on zeros and synchronises).
+ * Optional: forward calls grow it on demand, which synchronises; after a reservation
+ * no call up to that shape allocates device memory. */
 int zv_reserve(zv_handle h, int max_batch, int max_frames);
 /* Total bytes of device memory held (weights + workspace). */
 int64_t zv_device_bytes(zv_handle h);
@@ -128,6 +130,20 @@ int zv_velocity(zv_handle h, float t, float guidance_scale, const float* x,
 int zv_euler_sample(zv_handle h, float* x, const float* text_c, const float* speech_c,
                     const uint8_t* pad, int B, int T, int num_step, float guidance_scale,
                     float t_start, float t_end, float t_shift, void* stream);
+
+/* Per-utterance guidance scales (the reference's guidance_scale tensor of shape
+ * (batch, 1, 1), solver.py:61-62): guidance_rows is a device array of B floats.
+ * (guidance_rows == 0).all() selects the unguided branch (solver.py:71-79; one small
+ * device-to-host read at entry, as the reference's host predicate); otherwise CFG with
+ * g_b per row, doubled where t <= 0.5 (:95).  Distill: the rows feed the guidance
+ * embedding (solver.py:127-165). */
+int zv_velocity_rows(zv_handle h, float t, const float* guidance_rows, const float* x,
+                     const float* text_c, const float* speech_c, const uint8_t* pad, int B,
+                     int T, float* v_out, void* stream);
+int zv_euler_sample_rows(zv_handle h, float* x, const float* text_c, const float* speech_c,
+                         const uint8_t* pad, int B, int T, int num_step,
+                         const float* guidance_rows, float t_start, float t_end,
+                         float t_shift, void* stream);
 
 /* Text encoder (+ dialog speaker-turn embeddings).
  *  tokens: [B, S] int64 (already padded with pad_id, one extra pad per row);

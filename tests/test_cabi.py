@@ -64,3 +64,20 @@ def test_no_cpu_fallback():
         m.to("cuda:0")
     with pytest.raises(RuntimeError):
         m.to("cpu")
+
+
+def test_library_built_from_these_sources():
+    """Build provenance: the in-tree library carries the sha256 of the sources it was
+    compiled from (zv_version "src=..."); it must equal the hash of the current tree, so
+    a stale prebuilt .so cannot pass for the sources under test."""
+    from zipvoice_amd.csrc.build import build, library_hash, source_hash
+    build(verbose=False)
+    assert library_hash() == source_hash()
+
+
+@pytest.mark.gpu
+def test_gpu_box_library_provenance():
+    """On the GPU box (prebuilt library shipped with the tree, no rebuild): the library
+    the GPU tests load was compiled from the sources shipped beside it."""
+    from zipvoice_amd.csrc.build import library_hash, source_hash
+    assert library_hash() == source_hash(), "stale libzipvoice_hip.so"

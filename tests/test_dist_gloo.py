@@ -76,3 +76,64 @@ def test_all_gather_reassembles_batch_world2():
         for i in range(7):
             assert torch.all(allx[i, :costs[i]] == float(i))
             assert torch.all(allx[i, costs[i]:] == 0)
+
+
+def _dp_worker(rank, world, port, q):
+    """generate_batch_dp — the function bench.py's data-parallel step runs — with a CPU
+    compute stub in place of sample() + vocoder: utterance i yields costs[i] samples of
+    value i."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from zipvoice_amd.dist import generate_batch_dp
+        items = list(range(9))
+        costs = [5 + (3 * i) % 7 for i in items]
+        seen = []
+
+        def compute(shard):
+            seen.extend(shard)
+            n = max([costs[i] for i in shard], default=1)
+            wav = torch.zeros((len(shard), n))
+            for j, i in enumerate(shard):
+                wav[j, :costs[i]] = float(i)
+            return wav, torch.tensor([costs[i] for i in shard], dtype=torch.int64)
+
+        wav, lens, (lo, hi) = generate_batch_dp(items, compute, costs)
+        q.put((rank, wav.numpy().tolist(), lens.tolist(), seen, lo, hi))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_generate_batch_dp_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    costs = [5 + (3 * i) % 7 for i in range(9)]
+    # each rank computed exactly its own contiguous shard; together every item once
+    assert sorted(res[0][3] + res[1][3]) == list(range(9))
+    assert res[0][3] == list(range(res[0][4], res[0][5]))
+    assert res[0][5] == res[1][4]
+    for rank, wav, lens, _, _, _ in res:
+        assert lens == costs
+        wav = torch.tensor(wav)
+        assert wav.shape[0] == 9
+        for i in range(9):
+            assert torch.all(wav[i, :costs[i]] == float(i))
+            assert torch.all(wav[i, costs[i]:] == 0)
+
+
+def test_generate_batch_dp_single_process():
+    from zipvoice_amd.dist import generate_batch_dp
+    wav, lens, (lo, hi) = generate_batch_dp(
+        [0, 1, 2], lambda s: (torch.ones((len(s), 4)), torch.full((len(s),), 4)))
+    assert (lo, hi) == (0, 3) and wav.shape == (3, 4) and lens.tolist() == [4, 4, 4]
+    with pytest.raises(ValueError):
+        generate_batch_dp([0, 1], lambda s: (torch.ones((1, 4)), torch.ones(1)))

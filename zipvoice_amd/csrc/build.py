@@ -21,24 +21,56 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
+def source_hash(defines=()):
+    """sha256 over every source the library is built from (+ the extra defines): embedded
+    in the library (zv_version) so a prebuilt .so can be checked against the tree."""
+    import hashlib
+    h = hashlib.sha256()
+    for d in sorted(DEPS):
+        h.update(os.path.basename(d).encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    for d in defines:
+        h.update(d.encode())
+    return h.hexdigest()[:16]
+
+
+def library_hash(path=OUT):
+    """The source hash a built library carries (None if absent / unreadable)."""
+    import ctypes
+    if not os.path.exists(path):
+        return None
+    try:
+        v = ctypes.CDLL(path).zv_version
+        v.restype = ctypes.c_char_p
+        s = v().decode()
+    except OSError:
+        return None
+    return s.split("src=")[1].split()[0] if "src=" in s else None
+
+
 def up_to_date():
+    """Rebuild unless the in-tree library was built from exactly these sources."""
     if not os.path.exists(OUT):
         return False
-    t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(d) <= t for d in DEPS)
+    stamp = OUT + ".src"
+    return os.path.exists(stamp) and open(stamp).read().strip() == source_hash()
 
 
 def build(force=False, verbose=True, out=None, defines=()):
     if out is None and not force and up_to_date():
         return OUT
     out = out or OUT
+    digest = source_hash(defines)
     cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-munsafe-fp-atomics", "-Wno-unused-result", *[f"-D{d}" for d in defines],
-           "-o", out + ".tmp", SRC]
+           f'-DZV_SRC_HASH="{digest}"', "-o", out + ".tmp", SRC]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
     os.replace(out + ".tmp", out)
+    with open(out + ".src", "w") as f:
+        f.write(digest + "\n")
     return out
 
 

@@ -60,6 +60,7 @@ struct LayerW {
 struct StackW {
   int ds = 1;
   std::vector<LayerW> layers;
+  float* pos_w_all = nullptr;   // every layer's linear_pos weight, (layers, H*pd, pos_dim)
   Linear time_emb;          // fp32 small linear (time_embed_dim -> dim)
   float* ds_w = nullptr;    // softmax(downsample.bias)
   float* combiner = nullptr;
@@ -150,8 +151,6 @@ struct zv_engine {
   float* embed_table = nullptr;   // (vocab, text_embed_dim)
   float* spk_table = nullptr;     // (2, feat_dim)
   float* temb_freqs = nullptr;    // (time_embed_dim/2)
-  std::map<int, float*> pe_cache; // L -> (2L-1, pos_dim)
-  std::map<std::pair<const float*, int>, float*> posp_cache;   // (layer pos weight, L) -> (2L-1, H*pd)
   Workspace ws_dec, ws_txt;
 
   bool materialize_attn = false;   // A/B: ZV_ATTN_MATERIALIZE=1 keeps the W-materialising path
@@ -211,27 +210,39 @@ struct zv_engine {
   // (shape, schedule) on an engine-owned stream over engine-owned staging copies
   // of the inputs, then replayed with one hipGraphLaunch: the host launch cost
   // (which bounds small-batch / single-sentence latency) goes away.  The first
-  // call of a key runs uncaptured (it sizes the workspace and fills the
-  // positional caches, which synchronise); ZV_GRAPH=0 disables capture.
+  // call of a key runs uncaptured (it sizes the workspace); ZV_GRAPH=0 disables
+  // capture.  The cache is bounded (LRU over MAX_GRAPHS executable graphs, each
+  // destroyed on eviction), so a server with varying shapes does not grow it.
   struct GraphKey {
     int B, T, N, has_pad;
     float g, t0, t1, shift;
+    int cfg_mode;            // 0: scalar g; 1: per-row g with CFG; 2: per-row g without CFG
     unsigned long gen;
     bool operator<(const GraphKey& o) const {
-      return std::tie(B, T, N, has_pad, g, t0, t1, shift, gen) <
-             std::tie(o.B, o.T, o.N, o.has_pad, o.g, o.t0, o.t1, o.shift, o.gen);
+      return std::tie(B, T, N, has_pad, g, t0, t1, shift, cfg_mode, gen) <
+             std::tie(o.B, o.T, o.N, o.has_pad, o.g, o.t0, o.t1, o.shift, o.cfg_mode, o.gen);
     }
   };
-  std::map<GraphKey, hipGraphExec_t> graphs;
+  static constexpr size_t MAX_GRAPHS = 8, MAX_SEEN = 256;
+  struct GraphEntry { hipGraphExec_t exec; unsigned long last_use; };
+  std::map<GraphKey, GraphEntry> graphs;
   std::map<GraphKey, int> graph_seen;
+  unsigned long graph_clock = 0;
   hipStream_t gstream = nullptr;
   hipEvent_t gev_in = nullptr, gev_out = nullptr;
-  DBuf gx, gtc, gsc, gpad;
+  DBuf gx, gtc, gsc, gpad, ggrows;
   bool graphs_enabled = true;
 
   void drop_graphs() {
-    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
     graphs.clear();
+  }
+  void evict_lru_graph() {
+    auto victim = graphs.begin();
+    for (auto it = graphs.begin(); it != graphs.end(); ++it)
+      if (it->second.last_use < victim->second.last_use) victim = it;
+    ZV_CHECK(hipGraphExecDestroy(victim->second.exec));
+    graphs.erase(victim);
   }
 
   ~zv_engine() {
@@ -240,8 +251,6 @@ struct zv_engine {
     if (gev_in) (void)hipEventDestroy(gev_in);
     if (gev_out) (void)hipEventDestroy(gev_out);
     for (void* p : allocs) (void)hipFree(p);
-    for (auto& kv : pe_cache) (void)hipFree(kv.second);
-    for (auto& kv : posp_cache) (void)hipFree(kv.second);
   }
 
   // ---------------------------------------------------------------- weights
@@ -341,6 +350,7 @@ struct zv_engine {
     Z.qd = cfg.query_head_dim; Z.pd = cfg.pos_head_dim; Z.vd = cfg.value_head_dim;
     Z.pos_dim = cfg.pos_dim; Z.temb_dim = temb_dim;
     ZV_REQUIRE(Z.qd == ATT_QD && Z.pd == ATT_PD, "engine supports query_head_dim=32, pos_head_dim=4");
+    ZV_REQUIRE(Z.pos_dim % 2 == 0 && Z.pos_dim <= POSP_MAXD, "pos_dim must be even and <= 64");
     ZV_REQUIRE(heads * Z.vd <= 64, "num_heads * value_head_dim must be <= 64");
     for (size_t i = 0; i < in_dims.size(); ++i) {
       std::string s = two_stream ? "." + std::to_string(i) : "";
@@ -367,12 +377,17 @@ struct zv_engine {
         S.combiner = upload_f32(sp + "out_combiner.bypass_scale", dim);
       }
       if (temb_dim > 0) S.time_emb = make_small(ep + "time_emb.1", dim, temb_dim, true);
+      const size_t pw_n = (size_t)heads * Z.pd * Z.pos_dim;
+      S.pos_w_all = dalloc<float>(pw_n * std::max(layers[s], 1));
       for (int li = 0; li < layers[s]; ++li) {
         std::string lp = ep + "layers." + std::to_string(li) + ".";
         LayerW W;
         W.attn_in = make_linear(lp + "self_attn_weights.in_proj", qkp, dim, true, false);
-        W.pos_w = upload_f32(lp + "self_attn_weights.linear_pos.weight",
-                             (size_t)heads * Z.pd * Z.pos_dim);
+        {
+          const auto& pw = take(lp + "self_attn_weights.linear_pos.weight", pw_n);
+          W.pos_w = S.pos_w_all + li * pw_n;
+          ZV_CHECK(hipMemcpy(W.pos_w, pw.data(), pw_n * sizeof(float), hipMemcpyHostToDevice));
+        }
         for (int a = 0; a < 2; ++a) {
           std::string ap = lp + "self_attn" + std::to_string(a + 1) + ".";
           W.sa_in[a] = make_linear(ap + "in_proj", heads * Z.vd, dim, true, false);
@@ -469,35 +484,6 @@ struct zv_engine {
       return n;
     };
     return zf(dec) + zf(txt) + 1 + (dialog() ? 1 : 0);
-  }
-
-  // pe table for length L (CompactRelPositionalEncoding, zipformer.py:983-1056)
-  float* pe_table(int L, hipStream_t s) {
-    auto it = pe_cache.find(L);
-    if (it != pe_cache.end()) return it->second;
-    const int D = cfg.pos_dim, R = 2 * L - 1;
-    std::vector<float> pe((size_t)R * D, 0.f);
-    const double c = sqrt((double)D);
-    const float cf = (float)c, logc = (float)log(c);
-    const float length_scale = (float)(1.0 * D / (2.0 * M_PI));
-    for (int n = 0; n < R; ++n) {
-      const float x = (float)(n - (L - 1));
-      const float sg = x > 0 ? 1.f : (x < 0 ? -1.f : 0.f);
-      const float xc = cf * sg * (logf(fabsf(x) + cf) - logc);
-      const float xa = atanf(xc / length_scale);
-      for (int k = 0; k < D / 2; ++k) {
-        const float a = xa * (float)(k + 1);
-        pe[(size_t)n * D + 2 * k] = cosf(a);
-        pe[(size_t)n * D + 2 * k + 1] = sinf(a);
-      }
-      pe[(size_t)n * D + D - 1] = 1.f;
-    }
-    float* d = nullptr;
-    ZV_CHECK(hipMalloc(&d, pe.size() * sizeof(float)));
-    ZV_CHECK(hipMemcpyAsync(d, pe.data(), pe.size() * sizeof(float), hipMemcpyHostToDevice, s));
-    ZV_CHECK(hipStreamSynchronize(s));
-    pe_cache[L] = d;
-    return d;
   }
 
   // ---------------------------------------------------------------- launch helpers
@@ -606,26 +592,14 @@ struct zv_engine {
   // cur/cur_a: src + temb on entry (working residual stream).
   template <int SPLIT>
   void layer(const ZipformerW& Z, const LayerW& W, Workspace& ws, float* src, Act src_a,
-             float* cur, Act cur_a, int B, int L, const uint8_t* pad, const float* pe,
+             float* cur, Act cur_a, int B, int L, const uint8_t* pad, const float* posP,
              const float* temb, bool has_next, hipStream_t s) {
     const bool split = SPLIT == 3;
     const long M = (long)B * L;
     const int D = Z.dim, H = Z.heads;
     const long Lpad = round_up(L, 64);
     const char* tag_att = split ? "gemm_attn_fp32" : "gemm_attn_bf16";
-    // positional projection (2L-1, H*pd)
-    // depends only on (layer, L): computed once per length and kept (bounded)
-    if (posp_cache.size() > 1024 && !posp_cache.count({W.pos_w, L})) {
-      ZV_CHECK(hipStreamSynchronize(s));
-      for (auto& kv : posp_cache) ZV_CHECK(hipFree(kv.second));
-      posp_cache.clear();
-    }
-    float*& posP = posp_cache[{W.pos_w, L}];
-    if (!posP) {
-      ZV_CHECK(hipMalloc(&posP, (size_t)(2 * L - 1) * H * Z.pd * sizeof(float)));
-      Linear pl; pl.N = H * Z.pd; pl.K = Z.pos_dim; pl.w32 = W.pos_w;
-      small_linear(pl, pe, Z.pos_dim, 2 * L - 1, posP, H * Z.pd, 0, nullptr, s);
-    }
+    // posP: this layer's positional projection (2L-1, H*pd), written at stack entry
     // attention weights from the layer input (zipformer.py:526)
     const int qkpN = W.attn_in.N;
     Act qkp = ws.qkp.get(M, qkpN, split);
@@ -781,10 +755,17 @@ struct zv_engine {
     hipLaunchKernelGGL(zv_stack_entry_kernel, grid1d(M * Z.dim), dim3(256), 0, s, src, temb, cur,
                        src_a.h, src_a.l, cur_a.h, cur_a.l, (long)Z.dim, M, Z.dim, L);
     ZV_LAUNCH_CHECK();
-    const float* pe = pe_table(L, s);
+    // positional encoding of length L and every layer's linear_pos projection of it, in one
+    // launch into the workspace (zipformer.py:983-1056, :1239): no host table, no cache, no
+    // synchronisation, graph-capturable
+    const int R = 2 * L - 1, HPD = Z.heads * Z.pd, nl = (int)S.layers.size();
+    float* posP = ws.posP.get<float>((size_t)std::max(nl, 1) * R * HPD);
+    hipLaunchKernelGGL(zv_posp_kernel, grid1d((long)nl * R), dim3(256), 0, s, S.pos_w_all, posP,
+                       L, nl, HPD, Z.pos_dim);
+    ZV_LAUNCH_CHECK();
     for (size_t li = 0; li < S.layers.size(); ++li)
-      layer<SPLIT>(Z, S.layers[li], ws, src, src_a, cur, cur_a, B, L, pad, pe, temb,
-                   li + 1 < S.layers.size(), s);
+      layer<SPLIT>(Z, S.layers[li], ws, src, src_a, cur, cur_a, B, L, pad,
+                   posP + li * (size_t)R * HPD, temb, li + 1 < S.layers.size(), s);
   }
 
   // ---------------------------------------------------------------- TTSZipformer
@@ -871,20 +852,23 @@ struct zv_engine {
     else zipformer<1>(dec, ws_dec, xin, sidx, N, T, pad, t, g, out, s);
   }
 
-  // guided velocity at scalar t for B un-doubled rows (solver.py:40-165)
-  void velocity(float t, float gscale, const float* x, const float* tc, const float* sc,
-                const uint8_t* pad, int B, int T, float* vout, bool euler, float dt,
-                hipStream_t s) {
+  // guided velocity at scalar t for B un-doubled rows (solver.py:40-165).
+  // grows (device, B floats, may be null): per-utterance guidance scales, the reference's
+  // guidance_scale tensor of shape (batch, 1, 1); cfg_on says whether any is nonzero
+  // ((guidance_scale == 0.0).all() selects the unguided branch, solver.py:71)
+  void velocity(float t, float gscale, const float* grows, bool cfg_rows, const float* x,
+                const float* tc, const float* sc, const uint8_t* pad, int B, int T, float* vout,
+                bool euler, float dt, hipStream_t s) {
     const int Fx = stereo() ? 2 * cfg.feat_dim : cfg.feat_dim;
     const int Fin = 2 * Fx + cfg.feat_dim;
-    const bool cfg_on = !distill() && gscale != 0.0f;
+    const bool cfg_on = !distill() && (grows ? cfg_rows : gscale != 0.0f);
     const int copies = cfg_on ? 2 : 1;
     const int N = copies * B;
-    float g = gscale;
+    float g = gscale, gmul = 1.0f;
     int zero_speech = 0;
     if (cfg_on) {
       if (t > 0.5f) zero_speech = 1;
-      else g = gscale * 2.0f;
+      else { g = gscale * 2.0f; gmul = 2.0f; }
     }
     Act xin = build_xin(ws_dec, x, tc, sc, B, T, Fx, copies, zero_speech, s);
     const uint8_t* padN = pad;
@@ -897,38 +881,49 @@ struct zv_engine {
     }
     float* tv = ws_dec.tvec.get<float>(N);
     hipLaunchKernelGGL(zv_fill_kernel, dim3(cdiv(N, 256)), dim3(256), 0, s, tv, t, N);
-    float* gv = nullptr;
-    if (distill()) {
-      gv = ws_dec.gvec.get<float>(N);
-      hipLaunchKernelGGL(zv_fill_kernel, dim3(cdiv(N, 256)), dim3(256), 0, s, gv, gscale, N);
-    }
     ZV_LAUNCH_CHECK();
+    const float* gv = nullptr;
+    if (distill()) {
+      if (grows) {
+        gv = grows;   // the guidance embedding takes the per-row scales as they are
+      } else {
+        float* g1 = ws_dec.gvec.get<float>(N);
+        hipLaunchKernelGGL(zv_fill_kernel, dim3(cdiv(N, 256)), dim3(256), 0, s, g1, gscale, N);
+        ZV_LAUNCH_CHECK();
+        gv = g1;
+      }
+    }
     const long n = (long)B * T * Fx;
     float* v = (copies == 2 || euler) ? ws_dec.vout.get<float>((size_t)N * T * Fx) : vout;
     decoder(xin, Fin, N, T, padN, tv, gv, v, s);
+    const float* gr = cfg_on ? grows : nullptr;
     if (euler) {
       hipLaunchKernelGGL(zv_euler_update_kernel, grid1d(n), dim3(256), 0, s, const_cast<float*>(x),
-                         v, n, copies == 2 ? 1 : 0, g, dt);
+                         v, n, copies == 2 ? 1 : 0, g, dt, gr, gmul, (long)T * Fx);
       ZV_LAUNCH_CHECK();
     } else if (copies == 2) {
-      hipLaunchKernelGGL(zv_cfg_combine_kernel, grid1d(n), dim3(256), 0, s, vout, v, n, g);
+      hipLaunchKernelGGL(zv_cfg_combine_kernel, grid1d(n), dim3(256), 0, s, vout, v, n, g, gr,
+                         gmul, (long)T * Fx);
       ZV_LAUNCH_CHECK();
     }
   }
 
   void euler_loop(float* x, const float* tc, const float* sc, const uint8_t* pad, int B, int T,
-                  const std::vector<float>& ts, float g, hipStream_t s) {
+                  const std::vector<float>& ts, float g, const float* grows, bool cfg_rows,
+                  hipStream_t s) {
     const int num_step = (int)ts.size() - 1;
     for (int k = 0; k < num_step; ++k)
-      velocity(ts[k], g, x, tc, sc, pad, B, T, nullptr, true, ts[k + 1] - ts[k], s);
+      velocity(ts[k], g, grows, cfg_rows, x, tc, sc, pad, B, T, nullptr, true, ts[k + 1] - ts[k],
+               s);
   }
 
   // zv_euler_sample body: graph replay when possible, plain launches otherwise
   void euler_sample(float* x, const float* tc, const float* sc, const uint8_t* pad, int B, int T,
-                    int num_step, float g, float t0, float t1, float shift, hipStream_t s) {
+                    int num_step, float g, const float* grows, bool cfg_rows, float t0, float t1,
+                    float shift, hipStream_t s) {
     const std::vector<float> ts = time_steps(t0, t1, num_step, shift);
     if (!graphs_enabled || g_zv_prof.on) {
-      euler_loop(x, tc, sc, pad, B, T, ts, g, s);
+      euler_loop(x, tc, sc, pad, B, T, ts, g, grows, cfg_rows, s);
       return;
     }
     const int Fx = stereo() ? 2 * cfg.feat_dim : cfg.feat_dim;
@@ -938,11 +933,14 @@ struct zv_engine {
     float* stc = gtc.get<float>(nt);
     float* ssc = gsc.get<float>(nx);
     uint8_t* spad = pad ? gpad.get<uint8_t>((size_t)B * T) : nullptr;
-    GraphKey key{B, T, num_step, pad ? 1 : 0, g, t0, t1, shift, g_ws_generation};
+    float* sgr = grows ? ggrows.get<float>((size_t)B) : nullptr;
+    GraphKey key{B, T, num_step, pad ? 1 : 0, grows ? 0.f : g, t0, t1, shift,
+                 grows ? (cfg_rows ? 1 : 2) : 0, g_ws_generation};
     auto it = graphs.find(key);
     if (it == graphs.end() && graph_seen[key] == 0) {
-      graph_seen[key] = 1;                       // warm-up: sizes workspace, fills caches
-      euler_loop(x, tc, sc, pad, B, T, ts, g, s);
+      if (graph_seen.size() > MAX_SEEN) { graph_seen.clear(); graph_seen[key] = 0; }
+      graph_seen[key] = 1;                       // warm-up: sizes the workspace
+      euler_loop(x, tc, sc, pad, B, T, ts, g, grows, cfg_rows, s);
       return;
     }
     if (!gstream) {
@@ -956,13 +954,15 @@ struct zv_engine {
     ZV_CHECK(hipMemcpyAsync(stc, tc, nt * 4, hipMemcpyDeviceToDevice, gstream));
     ZV_CHECK(hipMemcpyAsync(ssc, sc, nx * 4, hipMemcpyDeviceToDevice, gstream));
     if (pad) ZV_CHECK(hipMemcpyAsync(spad, pad, (size_t)B * T, hipMemcpyDeviceToDevice, gstream));
+    if (grows) ZV_CHECK(hipMemcpyAsync(sgr, grows, (size_t)B * 4, hipMemcpyDeviceToDevice, gstream));
     if (it == graphs.end()) {
       if (key.gen != g_ws_generation) drop_graphs();
+      while (graphs.size() >= MAX_GRAPHS) evict_lru_graph();
       hipGraph_t graph = nullptr;
       ZV_CHECK(hipStreamBeginCapture(gstream, hipStreamCaptureModeThreadLocal));
       const unsigned long gen0 = g_ws_generation;
       try {
-        euler_loop(sx, stc, ssc, spad, B, T, ts, g, gstream);
+        euler_loop(sx, stc, ssc, spad, B, T, ts, g, sgr, cfg_rows, gstream);
       } catch (...) {
         (void)hipStreamEndCapture(gstream, &graph);
         if (graph) (void)hipGraphDestroy(graph);
@@ -973,9 +973,10 @@ struct zv_engine {
       hipGraphExec_t exec = nullptr;
       ZV_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
       ZV_CHECK(hipGraphDestroy(graph));
-      it = graphs.emplace(key, exec).first;
+      it = graphs.emplace(key, GraphEntry{exec, 0}).first;
     }
-    ZV_CHECK(hipGraphLaunch(it->second, gstream));
+    it->second.last_use = ++graph_clock;
+    ZV_CHECK(hipGraphLaunch(it->second.exec, gstream));
     ZV_CHECK(hipMemcpyAsync(x, sx, nx * 4, hipMemcpyDeviceToDevice, gstream));
     ZV_CHECK(hipEventRecord(gev_out, gstream));
     ZV_CHECK(hipStreamWaitEvent(s, gev_out, 0));
@@ -1083,7 +1084,10 @@ static float bench_variant8(GemmParams p, int iters, hipStream_t s) {
 extern "C" {
 
 const char* zv_last_error(void) { return g_last_error.c_str(); }
-const char* zv_version(void) { return "zipvoice_hip 0.1 (gfx950)"; }
+#ifndef ZV_SRC_HASH
+#define ZV_SRC_HASH "unknown"
+#endif
+const char* zv_version(void) { return "zipvoice_hip 0.2 (gfx950) src=" ZV_SRC_HASH; }
 
 zv_handle zv_create(const zv_config* cfg) {
   try {
@@ -1118,8 +1122,32 @@ int zv_finalize(zv_handle h) {
 int zv_reserve(zv_handle h, int max_batch, int max_frames) {
   ZV_API_BEGIN
   check_ready(h);
-  // touch the largest buffers once so later calls never reallocate
-  (void)max_batch; (void)max_frames;
+  ZV_REQUIRE(max_batch > 0 && max_frames > 0, "bad reservation");
+  // one uncaptured guided velocity at the largest shape sizes every decoder workspace
+  // buffer (CFG-doubled rows, positional projections, attention images), so later calls
+  // up to this shape never reallocate and captured graphs stay valid
+  const int Fx = h->stereo() ? 2 * h->cfg.feat_dim : h->cfg.feat_dim;
+  const size_t nx = (size_t)max_batch * max_frames * Fx;
+  const size_t nt = (size_t)max_batch * max_frames * h->cfg.feat_dim;
+  float *x = nullptr, *tc = nullptr, *v = nullptr;
+  uint8_t* pad = nullptr;
+  ZV_CHECK(hipMalloc(&x, nx * 4));
+  ZV_CHECK(hipMalloc(&tc, nt * 4));
+  ZV_CHECK(hipMalloc(&v, nx * 4));
+  ZV_CHECK(hipMalloc(&pad, (size_t)max_batch * max_frames));
+  ZV_CHECK(hipMemset(x, 0, nx * 4));
+  ZV_CHECK(hipMemset(tc, 0, nt * 4));
+  ZV_CHECK(hipMemset(pad, 0, (size_t)max_batch * max_frames));
+  auto release = [&]() { (void)hipFree(x); (void)hipFree(tc); (void)hipFree(v); (void)hipFree(pad); };
+  try {
+    h->velocity(0.25f, 1.0f, nullptr, false, x, tc, x, pad, max_batch, max_frames, v, false,
+                0.f, nullptr);
+    ZV_CHECK(hipDeviceSynchronize());
+  } catch (...) {
+    release();
+    throw;
+  }
+  release();
   ZV_API_END
 }
 
@@ -1303,7 +1331,8 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
 
 int64_t zv_device_bytes(zv_handle h) {
   if (!h) return 0;
-  return (int64_t)(h->weight_bytes + h->ws_dec.bytes() + h->ws_txt.bytes());
+  return (int64_t)(h->weight_bytes + h->ws_dec.bytes() + h->ws_txt.bytes() + h->gx.bytes +
+                   h->gtc.bytes + h->gsc.bytes + h->gpad.bytes + h->ggrows.bytes);
 }
 
 int zv_fm_decoder(zv_handle h, const float* t, const float* guidance, const float* xt,
@@ -1326,8 +1355,31 @@ int zv_velocity(zv_handle h, float t, float guidance_scale, const float* x, cons
   ZV_API_BEGIN
   check_ready(h);
   ZV_REQUIRE(B > 0 && T > 0, "empty batch");
-  h->velocity(t, guidance_scale, x, text_c, speech_c, pad, B, T, v_out, false, 0.f,
-              (hipStream_t)stream);
+  h->velocity(t, guidance_scale, nullptr, false, x, text_c, speech_c, pad, B, T, v_out, false,
+              0.f, (hipStream_t)stream);
+  ZV_API_END
+}
+
+// (guidance_scale == 0).all() of a device vector: one small D2H copy at API entry (the
+// reference evaluates the same predicate on the host every step, solver.py:71)
+static bool any_nonzero_rows(const float* grows, int B, hipStream_t s) {
+  std::vector<float> h(B);
+  ZV_CHECK(hipMemcpyAsync(h.data(), grows, (size_t)B * 4, hipMemcpyDeviceToHost, s));
+  ZV_CHECK(hipStreamSynchronize(s));
+  for (float v : h) if (v != 0.0f) return true;
+  return false;
+}
+
+int zv_velocity_rows(zv_handle h, float t, const float* guidance_rows, const float* x,
+                     const float* text_c, const float* speech_c, const uint8_t* pad, int B, int T,
+                     float* v_out, void* stream) {
+  ZV_API_BEGIN
+  check_ready(h);
+  ZV_REQUIRE(B > 0 && T > 0, "empty batch");
+  ZV_REQUIRE(guidance_rows != nullptr, "null guidance_rows");
+  hipStream_t s = (hipStream_t)stream;
+  const bool on = any_nonzero_rows(guidance_rows, B, s);
+  h->velocity(t, 0.f, guidance_rows, on, x, text_c, speech_c, pad, B, T, v_out, false, 0.f, s);
   ZV_API_END
 }
 
@@ -1337,8 +1389,23 @@ int zv_euler_sample(zv_handle h, float* x, const float* text_c, const float* spe
   ZV_API_BEGIN
   check_ready(h);
   ZV_REQUIRE(B > 0 && T > 0 && num_step > 0, "empty batch or zero steps");
-  h->euler_sample(x, text_c, speech_c, pad, B, T, num_step, guidance_scale, t_start, t_end,
-                  t_shift, (hipStream_t)stream);
+  h->euler_sample(x, text_c, speech_c, pad, B, T, num_step, guidance_scale, nullptr, false,
+                  t_start, t_end, t_shift, (hipStream_t)stream);
+  ZV_API_END
+}
+
+int zv_euler_sample_rows(zv_handle h, float* x, const float* text_c, const float* speech_c,
+                         const uint8_t* pad, int B, int T, int num_step,
+                         const float* guidance_rows, float t_start, float t_end, float t_shift,
+                         void* stream) {
+  ZV_API_BEGIN
+  check_ready(h);
+  ZV_REQUIRE(B > 0 && T > 0 && num_step > 0, "empty batch or zero steps");
+  ZV_REQUIRE(guidance_rows != nullptr, "null guidance_rows");
+  hipStream_t s = (hipStream_t)stream;
+  const bool on = any_nonzero_rows(guidance_rows, B, s);
+  h->euler_sample(x, text_c, speech_c, pad, B, T, num_step, 0.f, guidance_rows, on, t_start,
+                  t_end, t_shift, s);
   ZV_API_END
 }
 

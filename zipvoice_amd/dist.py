@@ -9,7 +9,7 @@ padded outputs, which reassembles the batch in its original order on every rank.
 """
 from __future__ import annotations
 
-from typing import List, Sequence, Tuple
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -67,3 +67,36 @@ def all_gather_padded(x: torch.Tensor, lens: torch.Tensor, group=None):
     rows = [o[:s[0]] for o, s in zip(outs, shapes)]
     lrows = [l[:s[0]] for l, s in zip(louts, shapes)]
     return torch.cat(rows, 0), torch.cat(lrows, 0)
+
+
+def _world_rank(group=None) -> Tuple[int, int]:
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+def generate_batch_dp(items: Sequence, compute: Callable[[Sequence], Tuple[torch.Tensor, torch.Tensor]],
+                      costs: Optional[Sequence[float]] = None, group=None):
+    """Data-parallel generation of one GLOBAL batch, the multi-GPU replacement of the
+    reference's single-device sentence loop (``infer_zipvoice.py:568-577``, ``:431-452``).
+
+    Every rank holds the same ``items`` list (one entry per utterance).  Rank r takes its
+    contiguous cost-balanced shard (:func:`shard_bounds` over ``costs``, e.g. frames per
+    utterance), runs ``compute(shard) -> (wav (b, n), lens (b,))`` on its own GPU (the
+    whole ``sample()`` + vocoder path; nothing crosses ranks inside it), and the single
+    exchange of the path, :func:`all_gather_padded` (RCCL over xGMI on GPUs, gloo on CPU),
+    reassembles the (B, n_max) wav batch and its lengths in the original item order on
+    every rank.  Returns (wav, lens, (lo, hi)) with (lo, hi) this rank's shard."""
+    world, rank = _world_rank(group)
+    if costs is None:
+        costs = [1.0] * len(items)
+    if len(costs) != len(items):
+        raise ValueError("costs must have one entry per item")
+    lo, hi = shard_bounds(costs, world)[rank]
+    wav, lens = compute(items[lo:hi])
+    if wav.dim() != 2 or lens.dim() != 1 or wav.shape[0] != lens.shape[0] or wav.shape[0] != hi - lo:
+        raise ValueError("compute must return (wav (b, n), lens (b,)) for its b = hi - lo items")
+    if world == 1:
+        return wav, lens, (lo, hi)
+    out, olens = all_gather_padded(wav.unsqueeze(-1), lens, group)
+    return out.squeeze(-1), olens, (lo, hi)

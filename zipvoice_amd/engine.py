@@ -66,6 +66,8 @@ SIGNATURES = {
     "zv_fm_decoder": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
     "zv_velocity": (_I, [_P, _F, _F, _P, _P, _P, _P, _I, _I, _P, _P]),
     "zv_euler_sample": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _F, _P]),
+    "zv_velocity_rows": (_I, [_P, _F, _P, _P, _P, _P, _P, _I, _I, _P, _P]),
+    "zv_euler_sample_rows": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _F, _F, _F, _P]),
     "zv_text_encode": (_I, [_P, _P, _P, _P, _I, _I, _P, _P]),
     "zv_text_condition": (_I, [_P, _P, _I, _I, _P, _P, _I, _P, _P]),
     "zv_speech_condition": (_I, [_P, _P, _I, _I, _I, _P, _I, _P, _P]),
@@ -250,7 +252,17 @@ class HipEngine:
                                       _ptr(speech_c), _ptr(pm), N, T, Fx, _ptr(v), _stream()))
         return v
 
-    def velocity(self, t: float, guidance_scale: float, x, text_c, speech_c,
+    def _guidance_rows(self, guidance_scale, B: int) -> Optional[torch.Tensor]:
+        """None for a scalar guidance scale; else the (B,) fp32 device vector of a
+        per-utterance guidance tensor ((batch, 1, 1) in the reference, solver.py:61-62)."""
+        if not torch.is_tensor(guidance_scale) or guidance_scale.numel() == 1:
+            return None
+        if guidance_scale.numel() != B:
+            raise ValueError(f"guidance_scale: expected 1 or {B} values (shape (batch, 1, 1)), "
+                             f"got shape {tuple(guidance_scale.shape)}")
+        return guidance_scale.reshape(B).to(self.device, torch.float32).contiguous()
+
+    def velocity(self, t: float, guidance_scale, x, text_c, speech_c,
                  padding_mask=None) -> torch.Tensor:
         B, T, Fx = x.shape
         x = self._f32(x, "x")
@@ -258,22 +270,39 @@ class HipEngine:
         speech_c = self._f32(speech_c, "speech_condition", (B, T, Fx))
         pm = self._mask(padding_mask, (B, T))
         v = torch.empty_like(x)
-        _check(self.lib.zv_velocity(self.h, float(t), float(guidance_scale), _ptr(x),
-                                    _ptr(text_c), _ptr(speech_c), _ptr(pm), B, T, _ptr(v),
-                                    _stream()))
+        gr = self._guidance_rows(guidance_scale, B)
+        if gr is not None:
+            _check(self.lib.zv_velocity_rows(self.h, float(t), _ptr(gr), _ptr(x), _ptr(text_c),
+                                             _ptr(speech_c), _ptr(pm), B, T, _ptr(v), _stream()))
+        else:
+            _check(self.lib.zv_velocity(self.h, float(t), float(guidance_scale), _ptr(x),
+                                        _ptr(text_c), _ptr(speech_c), _ptr(pm), B, T, _ptr(v),
+                                        _stream()))
         return v
 
     def euler_sample(self, x0, text_c, speech_c, padding_mask, num_step: int,
-                     guidance_scale: float, t_start=0.0, t_end=1.0, t_shift=1.0) -> torch.Tensor:
+                     guidance_scale, t_start=0.0, t_end=1.0, t_shift=1.0) -> torch.Tensor:
         B, T, Fx = x0.shape
         x = self._f32(x0, "x").clone()
         text_c = self._f32(text_c, "text_condition", (B, T, self.cfg.feat_dim))
         speech_c = self._f32(speech_c, "speech_condition", (B, T, Fx))
         pm = self._mask(padding_mask, (B, T))
-        _check(self.lib.zv_euler_sample(self.h, _ptr(x), _ptr(text_c), _ptr(speech_c), _ptr(pm),
-                                        B, T, int(num_step), float(guidance_scale),
-                                        float(t_start), float(t_end), float(t_shift), _stream()))
+        gr = self._guidance_rows(guidance_scale, B)
+        if gr is not None:
+            _check(self.lib.zv_euler_sample_rows(self.h, _ptr(x), _ptr(text_c), _ptr(speech_c),
+                                                 _ptr(pm), B, T, int(num_step), _ptr(gr),
+                                                 float(t_start), float(t_end), float(t_shift),
+                                                 _stream()))
+        else:
+            _check(self.lib.zv_euler_sample(self.h, _ptr(x), _ptr(text_c), _ptr(speech_c),
+                                            _ptr(pm), B, T, int(num_step), float(guidance_scale),
+                                            float(t_start), float(t_end), float(t_shift),
+                                            _stream()))
         return x
+
+    def reserve(self, max_batch: int, max_frames: int) -> None:
+        """Pre-size the decoder workspace (zv_reserve)."""
+        _check(self.lib.zv_reserve(self.h, int(max_batch), int(max_frames)))
 
     def text_encode(self, tokens: torch.Tensor, padding_mask: torch.Tensor,
                     spk: Optional[torch.Tensor] = None) -> torch.Tensor:

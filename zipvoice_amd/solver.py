@@ -26,14 +26,15 @@ class EulerSolver:
                speech_condition: torch.Tensor, padding_mask: torch.Tensor, num_step: int = 10,
                guidance_scale: Union[float, torch.Tensor] = 0.0, t_start: float = 0.0,
                t_end: float = 1.0, t_shift: float = 1.0, **kwargs) -> torch.Tensor:
+        """guidance_scale: a float or a tensor of shape (batch, 1, 1) (solver.py:61-62):
+        per-utterance scales run the same CFG loop with g per row."""
         assert isinstance(t_start, float) and isinstance(t_end, float)
-        if torch.is_tensor(guidance_scale):
-            if guidance_scale.numel() != 1:
-                raise NotImplementedError("per-utterance guidance scales are not supported")
+        if torch.is_tensor(guidance_scale) and guidance_scale.numel() == 1:
+            guidance_scale = float(guidance_scale)
+        if not torch.is_tensor(guidance_scale):
             guidance_scale = float(guidance_scale)
         return self.model.engine.euler_sample(x, text_condition, speech_condition, padding_mask,
-                                              num_step, float(guidance_scale), t_start, t_end,
-                                              t_shift)
+                                              num_step, guidance_scale, t_start, t_end, t_shift)
 
 
 class DistillEulerSolver(EulerSolver):
