@@ -20,6 +20,7 @@
 #include "zv_gemm.inc"
 #include "zv_gemm_ws.inc"
 #include "zv_gemm8.inc"
+#include "zv_gemm_pp.inc"
 #include "zv_attn.inc"
 #include "zv_elem.inc"
 #include "zv_flash.inc"
@@ -159,6 +160,9 @@ struct zv_engine {
   // one tile per block (gridx -1), the others persistent over the resident grid (0).
   int occ_plain = 2, occ_resid = 2, occ_fused = 2;
   int gridx_plain = 0, gridx_resid = -1, gridx_fused = 0;
+  int gemm_pp = 1;                 // ZV_GEMM_PP: bf16 linears with N % 128 == 0 (and the GLU / NA
+                                   // in-projections) on the ping-pong kernel (zv_gemm_pp.inc);
+                                   // 0 = the 128x128 kernels (A/B arm, bitwise equal)
   int resid_ws = 1;                // residual linears on the wave-specialised epilogue kernel:
                                    // ZV_RESID_WS 1 = K <= 64 only (default), 2 = all, 0 = none
   bool sa_pos_mfma = false;        // A/B: ZV_SA_POS_MFMA=1 puts the SelfAttention positional term on
@@ -204,6 +208,7 @@ struct zv_engine {
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
     resid_ws = envi("ZV_RESID_WS", 1);
+    gemm_pp = envi("ZV_GEMM_PP", 1);
   }
   // ---------------------------------------------------------------- HIP graphs
   // The whole N-step Euler solve (~250 launches per step) is captured once per
@@ -539,6 +544,14 @@ struct zv_engine {
       return;
     }
     if constexpr (SPLIT == 1) {
+      if (gemm_pp && Lw.N % 128 == 0 && !o.act.l && !o.residh && A.ld % 8 == 0 &&
+          (!o.C || o.ldc % 8 == 0) && (!o.act.h || o.act.ld % 8 == 0)) {
+        if (o.resid) launch_gemm_pp<128, 128, 3, EPI_STD, 1>(p, s, "gemm_bf16_resid");
+        else launch_gemm_pp<128, 128, 3, EPI_STD, 0>(p, s, "gemm_bf16");
+        return;
+      }
+    }
+    if constexpr (SPLIT == 1) {
       if (gemm_tile == 1 && Lw.N >= 256) {
         launch_gemm<256, 128, 4, 2, SPLIT, EPI_STD>(p, 1, s, tag);
         return;
@@ -643,7 +656,9 @@ struct zv_engine {
       p.Cth = xt.h; p.Ctl = xt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)hid * Lpad;
       bool done = false;
       if constexpr (SPLIT == 1)
-        if (fused_tile == 1) { launch_gemm<256, 96, 4, 2, SPLIT, EPI_NA, 2, 2>(p, 1, s, "gemm_bf16_na"); done = true; }
+        if (gemm_pp && W.na_in.N % 96 == 0) { launch_gemm_pp<128, 96, 3, EPI_NA, 0>(p, s, "gemm_bf16_na"); done = true; }
+      if constexpr (SPLIT == 1)
+        if (!done && fused_tile == 1) { launch_gemm<256, 96, 4, 2, SPLIT, EPI_NA, 2, 2>(p, 1, s, "gemm_bf16_na"); done = true; }
       if (done) {}
       else if (occ_fused == 2) launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       else launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 1>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
@@ -705,7 +720,9 @@ struct zv_engine {
       p.Ch = g.h; p.Cl = g.l; p.ldch = g.ld; p.rowmask = pad;
       bool done = false;
       if constexpr (SPLIT == 1)
-        if (fused_tile == 1) { launch_gemm<256, 128, 4, 2, SPLIT, EPI_GLU, 3>(p, 1, s, "gemm_bf16_glu"); done = true; }
+        if (gemm_pp && W.conv_in[c].N % 128 == 0) { launch_gemm_pp<128, 128, 3, EPI_GLU, 0>(p, s, "gemm_bf16_glu"); done = true; }
+      if constexpr (SPLIT == 1)
+        if (!done && fused_tile == 1) { launch_gemm<256, 128, 4, 2, SPLIT, EPI_GLU, 3>(p, 1, s, "gemm_bf16_glu"); done = true; }
       if (done) {}
       else if (occ_fused == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       else launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 1>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
@@ -1066,6 +1083,21 @@ static float bench_variant(GemmParams p, int iters, bool persistent, hipStream_t
   return ms / iters;
 }
 
+template <int BM, int BN, int STAGES, int EPI>
+static float bench_variant_pp(GemmParams p, int iters, hipStream_t s) {
+  hipEvent_t e0, e1;
+  ZV_CHECK(hipEventCreate(&e0)); ZV_CHECK(hipEventCreate(&e1));
+  launch_gemm_pp<BM, BN, STAGES, EPI, 0>(p, s, "bench");
+  ZV_CHECK(hipEventRecord(e0, s));
+  for (int i = 0; i < iters; ++i) launch_gemm_pp<BM, BN, STAGES, EPI, 0>(p, s, "bench");
+  ZV_CHECK(hipEventRecord(e1, s));
+  ZV_CHECK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  ZV_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  ZV_CHECK(hipEventDestroy(e0)); ZV_CHECK(hipEventDestroy(e1));
+  return ms / iters;
+}
+
 template <int ORDER, bool PB>
 static float bench_variant8(GemmParams p, int iters, hipStream_t s) {
   hipEvent_t e0, e1;
@@ -1139,6 +1171,12 @@ int zv_reserve(zv_handle h, int max_batch, int max_frames) {
   ZV_CHECK(hipMemset(tc, 0, nt * 4));
   ZV_CHECK(hipMemset(pad, 0, (size_t)max_batch * max_frames));
   auto release = [&]() { (void)hipFree(x); (void)hipFree(tc); (void)hipFree(v); (void)hipFree(pad); };
+  // the graph path's staging copies of the inputs, too
+  (void)h->gx.get<float>(nx);
+  (void)h->gtc.get<float>(nt);
+  (void)h->gsc.get<float>(nx);
+  (void)h->gpad.get<uint8_t>((size_t)max_batch * max_frames);
+  (void)h->ggrows.get<float>((size_t)max_batch);
   try {
     h->velocity(0.25f, 1.0f, nullptr, false, x, tc, x, pad, max_batch, max_frames, v, false,
                 0.f, nullptr);
@@ -1234,6 +1272,8 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
     case 21: ms = bench_variant8<1, true>(p, iters, s); break;
     case 22: ms = bench_variant8<0, false>(p, iters, s); break;
     case 23: ms = bench_variant8<1, false>(p, iters, s); break;
+    case 50: ms = bench_variant_pp<128, 128, 3, EPI_STD>(p, iters, s); break;
+    case 51: ms = bench_variant_pp<128, 128, 2, EPI_STD>(p, iters, s); break;
     default: throw std::invalid_argument("unknown variant");
   }
   *ms_out = ms;
@@ -1313,6 +1353,8 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
       case 21: launch_gemm8<1, EPI_STD, true>(p, s, "t"); break;
       case 22: launch_gemm8<0, EPI_STD, false>(p, s, "t"); break;
       case 23: launch_gemm8<1, EPI_STD, false>(p, s, "t"); break;
+      case 50: launch_gemm_pp<128, 128, 3, EPI_STD, 0>(p, s, "t"); break;
+      case 51: launch_gemm_pp<128, 128, 2, EPI_STD, 0>(p, s, "t"); break;
       default: throw std::invalid_argument("selftest: unknown variant");
     }
   }
