@@ -546,8 +546,8 @@ struct zv_engine {
     if constexpr (SPLIT == 1) {
       if (gemm_pp && Lw.N % 128 == 0 && !o.act.l && !o.residh && A.ld % 8 == 0 &&
           (!o.C || o.ldc % 8 == 0) && (!o.act.h || o.act.ld % 8 == 0)) {
-        if (o.resid) launch_gemm_pp<128, 128, 3, EPI_STD, 1>(p, s, "gemm_bf16_resid");
-        else launch_gemm_pp<128, 128, 3, EPI_STD, 0>(p, s, "gemm_bf16");
+        if (o.resid) launch_gemm_pp<128, 128, 2, 4, EPI_STD, 1>(p, s, "gemm_bf16_resid");
+        else launch_gemm_pp<128, 128, 2, 4, EPI_STD, 0>(p, s, "gemm_bf16");
         return;
       }
     }
@@ -656,7 +656,7 @@ struct zv_engine {
       p.Cth = xt.h; p.Ctl = xt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)hid * Lpad;
       bool done = false;
       if constexpr (SPLIT == 1)
-        if (gemm_pp && W.na_in.N % 96 == 0) { launch_gemm_pp<128, 96, 3, EPI_NA, 0>(p, s, "gemm_bf16_na"); done = true; }
+        if (gemm_pp && W.na_in.N % 192 == 0) { launch_gemm_pp<128, 192, 2, 4, EPI_NA, 0>(p, s, "gemm_bf16_na"); done = true; }
       if constexpr (SPLIT == 1)
         if (!done && fused_tile == 1) { launch_gemm<256, 96, 4, 2, SPLIT, EPI_NA, 2, 2>(p, 1, s, "gemm_bf16_na"); done = true; }
       if (done) {}
@@ -720,7 +720,7 @@ struct zv_engine {
       p.Ch = g.h; p.Cl = g.l; p.ldch = g.ld; p.rowmask = pad;
       bool done = false;
       if constexpr (SPLIT == 1)
-        if (gemm_pp && W.conv_in[c].N % 128 == 0) { launch_gemm_pp<128, 128, 3, EPI_GLU, 0>(p, s, "gemm_bf16_glu"); done = true; }
+        if (gemm_pp && W.conv_in[c].N % 128 == 0) { launch_gemm_pp<128, 128, 2, 4, EPI_GLU, 0>(p, s, "gemm_bf16_glu"); done = true; }
       if constexpr (SPLIT == 1)
         if (!done && fused_tile == 1) { launch_gemm<256, 128, 4, 2, SPLIT, EPI_GLU, 3>(p, 1, s, "gemm_bf16_glu"); done = true; }
       if (done) {}
@@ -1083,13 +1083,13 @@ static float bench_variant(GemmParams p, int iters, bool persistent, hipStream_t
   return ms / iters;
 }
 
-template <int BM, int BN, int STAGES, int EPI>
+template <int BM, int BN, int WGM, int WGN, int EPI>
 static float bench_variant_pp(GemmParams p, int iters, hipStream_t s) {
   hipEvent_t e0, e1;
   ZV_CHECK(hipEventCreate(&e0)); ZV_CHECK(hipEventCreate(&e1));
-  launch_gemm_pp<BM, BN, STAGES, EPI, 0>(p, s, "bench");
+  launch_gemm_pp<BM, BN, WGM, WGN, EPI, 0>(p, s, "bench");
   ZV_CHECK(hipEventRecord(e0, s));
-  for (int i = 0; i < iters; ++i) launch_gemm_pp<BM, BN, STAGES, EPI, 0>(p, s, "bench");
+  for (int i = 0; i < iters; ++i) launch_gemm_pp<BM, BN, WGM, WGN, EPI, 0>(p, s, "bench");
   ZV_CHECK(hipEventRecord(e1, s));
   ZV_CHECK(hipEventSynchronize(e1));
   float ms = 0.f;
@@ -1272,8 +1272,7 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
     case 21: ms = bench_variant8<1, true>(p, iters, s); break;
     case 22: ms = bench_variant8<0, false>(p, iters, s); break;
     case 23: ms = bench_variant8<1, false>(p, iters, s); break;
-    case 50: ms = bench_variant_pp<128, 128, 3, EPI_STD>(p, iters, s); break;
-    case 51: ms = bench_variant_pp<128, 128, 2, EPI_STD>(p, iters, s); break;
+    case 50: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD>(p, iters, s); break;
     default: throw std::invalid_argument("unknown variant");
   }
   *ms_out = ms;
@@ -1353,8 +1352,7 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
       case 21: launch_gemm8<1, EPI_STD, true>(p, s, "t"); break;
       case 22: launch_gemm8<0, EPI_STD, false>(p, s, "t"); break;
       case 23: launch_gemm8<1, EPI_STD, false>(p, s, "t"); break;
-      case 50: launch_gemm_pp<128, 128, 3, EPI_STD, 0>(p, s, "t"); break;
-      case 51: launch_gemm_pp<128, 128, 2, EPI_STD, 0>(p, s, "t"); break;
+      case 50: launch_gemm_pp<128, 128, 2, 4, EPI_STD, 0>(p, s, "t"); break;
       default: throw std::invalid_argument("selftest: unknown variant");
     }
   }
