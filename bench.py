@@ -325,6 +325,19 @@ def main():
                 "note": "bf16x3 split-product GEMMs; the parity mode (mean |err| ~3e-5 vs reference); "
                         "timed after 2 warm-up steps"}
             del job32, m32
+            torch.cuda.empty_cache()
+            m16 = build(conf["variant"], "fp16", device)
+            job16 = Job(conf, m16, vocoder, n_items, device)
+            ms16 = timed(job16, args.steps, 2, 1) * 1e3
+            result["fp16_parity_mode"] = {
+                "ms_per_step": round(ms16, 2),
+                "value": round(frames / (ms16 * 1e-3), 1), "unit": "mel-frames/s",
+                "vs_bf16_time": round(ms16 / ms, 3),
+                "note": "fp16 MFMA operands in the decoder layers, split products for the "
+                        "decoder in/out projections and the text encoder: meets the north-star "
+                        "1e-3 mean |err| bar (tests/test_gpu_parity.py, test_gpu_fullsize.py); "
+                        "timed after 2 warm-up steps"}
+            del job16, m16
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(conf["variant"], conf["guidance"],
                                                   conf["num_step"])

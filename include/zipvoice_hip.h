@@ -49,9 +49,16 @@ extern "C" {
 typedef struct zv_engine* zv_handle;
 
 enum zv_variant { ZV_ZIPVOICE = 0, ZV_DISTILL = 1, ZV_DIALOG = 2, ZV_DIALOG_STEREO = 3 };
-/* ZV_FP32: fp32-accurate mode (GEMMs as bf16x3 split products, fp32 everything else);
- * ZV_BF16: bf16 MFMA operands, fp32 accumulation / residual stream / softmax. */
-enum zv_precision { ZV_FP32 = 0, ZV_BF16 = 1 };
+/* ZV_FP32: fp32-accurate mode (GEMMs as split products hi*hi + hi*lo + lo*hi of 16-bit
+ *          operands, fp32 everything else);
+ * ZV_BF16: 16-bit MFMA operands, fp32 accumulation / residual stream / softmax;
+ * ZV_MIXED: ZV_BF16 for the decoder layers, the split products for the decoder's input /
+ *          output projections and the whole text encoder (the cheap linears that carry most
+ *          of the 16-bit rounding error into the output).
+ * The 16-bit operand format is the library's: bf16 in libzipvoice_hip.so, IEEE fp16 in
+ * libzipvoice_hip_f16.so (same entry points, built from the same sources with
+ * -DZV_OPERAND_F16).  ZV_MIXED in the fp16 library is the parity-grade fast mode. */
+enum zv_precision { ZV_FP32 = 0, ZV_BF16 = 1, ZV_MIXED = 2 };
 
 #define ZV_MAX_STACKS 8
 

@@ -67,17 +67,32 @@ def test_no_cpu_fallback():
 
 
 def test_library_built_from_these_sources():
-    """Build provenance: the in-tree library carries the sha256 of the sources it was
-    compiled from (zv_version "src=..."); it must equal the hash of the current tree, so
-    a stale prebuilt .so cannot pass for the sources under test."""
-    from zipvoice_amd.csrc.build import build, library_hash, source_hash
+    """Build provenance: each in-tree library (bf16 and fp16 operand builds) carries the
+    sha256 of the sources it was compiled from (zv_version "src=..."); it must equal the hash
+    of the current tree, so a stale prebuilt .so cannot pass for the sources under test."""
+    from zipvoice_amd.csrc.build import VARIANTS, build, library_hash, source_hash
     build(verbose=False)
-    assert library_hash() == source_hash()
+    for out, defines in VARIANTS:
+        assert library_hash(out) == source_hash(defines), out
+
+
+def test_both_operand_libraries_load_side_by_side():
+    """The bf16- and fp16-operand engines export the same entry points; both load into one
+    process (RTLD_LOCAL, -Bsymbolic) and each answers for itself."""
+    from zipvoice_amd import engine
+    a = engine.load_library()
+    b = engine.load_library(operand="f16")
+    assert a is not b
+    va, vb = a.zv_version().decode(), b.zv_version().decode()
+    assert "bf16 operands" in va and "fp16 operands" in vb, (va, vb)
+    for name in engine.SIGNATURES:
+        assert hasattr(b, name), name
 
 
 @pytest.mark.gpu
 def test_gpu_box_library_provenance():
     """On the GPU box (prebuilt library shipped with the tree, no rebuild): the library
     the GPU tests load was compiled from the sources shipped beside it."""
-    from zipvoice_amd.csrc.build import library_hash, source_hash
-    assert library_hash() == source_hash(), "stale libzipvoice_hip.so"
+    from zipvoice_amd.csrc.build import VARIANTS, library_hash, source_hash
+    for out, defines in VARIANTS:
+        assert library_hash(out) == source_hash(defines), f"stale {out}"

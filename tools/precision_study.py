@@ -59,6 +59,7 @@ class Emu:
     def __init__(self, fam):
         self.fam = fam          # dict family -> format (None = fp32)
         self.cur = "io"
+        self.text_exact = False  # text encoder left in fp32
 
     def q(self, x, fam=None):
         return QF[self.fam.get(fam or self.cur)](x)
@@ -83,7 +84,7 @@ def linear(x, w, b=None):
 def attn_weights(P, x, pe, key_pad, heads, qdim, pdim):
     prev, EMU.cur = EMU.cur, "attn"
     B, L, _ = x.shape
-    xp = EMU.q(linear(x, P["in_proj.weight"], P["in_proj.bias"]))   # q | k | p stored 16-bit
+    xp = EMU.q(linear(x, P["in_proj.weight"], P["in_proj.bias"]), "qk")   # q | k | p stored 16-bit
     EMU.cur = prev
     qd = qdim * heads
     qq = xp[..., :qd].reshape(B, L, heads, qdim).transpose(2, 0, 1, 3)
@@ -155,7 +156,18 @@ def conv_module(P, x, key_pad):
     return out
 
 
+def _text_embed_exact(orig):
+    def f(self, tokens):
+        saved, EMU.fam = EMU.fam, ({} if EMU.text_exact else EMU.fam)
+        try:
+            return orig(self, tokens)
+        finally:
+            EMU.fam = saved
+    return f
+
+
 def install():
+    Z.ZipVoiceOracle.forward_text_embed = _text_embed_exact(Z.ZipVoiceOracle.forward_text_embed)
     Z.linear = linear
     Z.attn_weights = attn_weights
     Z.feed_forward = feed_forward
@@ -179,6 +191,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r02_precision_study.txt"))
     ap.add_argument("--fixture", default="sample_c1.npz")
+    ap.add_argument("--mixed", action="store_true")
     args = ap.parse_args()
     from zipvoice_amd.config import default_config
     from zipvoice_amd.weights import synthetic_state_dict
@@ -187,7 +200,16 @@ def main():
     cfg = default_config(str(d["variant"]))
     o = Z.ZipVoiceOracle(cfg, synthetic_state_dict(cfg, 0))
     KEYS.update({id(v): k for k, v in o.sd.items()})
-    fams = ["attn", "ff", "na", "sa", "conv", "io"]
+    fams = ["attn", "qk", "ff", "na", "sa", "conv", "io"]
+    if "--mixed" in sys.argv:
+        arms = []
+        base = {g: "fp16" for g in fams}
+        for keep in (["io"], ["io", "attn"], ["io", "qk"], ["io", "attn", "qk"], ["io", "sa"]):
+            for tx in (False, True):
+                arms.append((f"{'+'.join(keep)} fp32, rest fp16{' +text fp32' if tx else ''}",
+                             dict(base, **{g: None for g in keep}), tx))
+        run_arms(o, d, arms, args.out.replace(".txt", "_mixed.txt"))
+        return
     arms = [("fp32 (emulation off)", {})]
     arms.append(("all bf16", {f: "bf16" for f in fams}))
     arms.append(("all fp16", {f: "fp16" for f in fams}))
@@ -202,19 +224,24 @@ def main():
         for fmt in ("bf16", "fp16"):
             arms.append((f"{'+'.join(keep)} fp32, rest {fmt}",
                          {g: (None if g in keep else fmt) for g in fams}))
-    lines = [f"# precision study: oracle with emulated MFMA-operand rounding; fixture {args.fixture} "
-             f"(reference fp32 output); metric = mean / max |gen - ref| (and prompt part)"]
-    for name, fam in arms:
+    run_arms(o, d, [(n, f, False) for n, f in arms], args.out)
+
+
+def run_arms(o, d, arms, out):
+    lines = ["# precision study: oracle with emulated MFMA-operand rounding; fixture sample_c1 "
+             "(reference fp32 output); metric = mean / max |gen - ref| (and prompt part)"]
+    for name, fam, tx in arms:
         EMU.fam = fam
+        EMU.text_exact = tx
         t0 = time.time()
         gen, prm = run_sample(o, d)
         eg = np.abs(gen - d["gen"])
         ep = np.abs(prm - d["prompt"])
-        line = (f"{name:32s} gen mean {eg.mean():.3e} max {eg.max():.3e} | prompt mean "
+        line = (f"{name:40s} gen mean {eg.mean():.3e} max {eg.max():.3e} | prompt mean "
                 f"{ep.mean():.3e} max {ep.max():.3e}   ({time.time() - t0:.1f} s)")
         print(line, flush=True)
         lines.append(line)
-    with open(args.out, "w") as f:
+    with open(out, "w") as f:
         f.write("\n".join(lines) + "\n")
 
 

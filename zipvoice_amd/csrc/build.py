@@ -8,6 +8,9 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 OUT = os.path.join(PKG, "libzipvoice_hip.so")
+# the same sources with fp16 MFMA operands (the parity-grade fast mode's library)
+OUT_F16 = os.path.join(PKG, "libzipvoice_hip_f16.so")
+VARIANTS = ((OUT, ()), (OUT_F16, ("ZV_OPERAND_F16",)))
 SRC = os.path.join(HERE, "zv_engine.hip")
 DEPS = [os.path.join(HERE, f) for f in os.listdir(HERE)
         if f.endswith((".hip", ".inc", ".h"))] + [
@@ -49,29 +52,40 @@ def library_hash(path=OUT):
     return s.split("src=")[1].split()[0] if "src=" in s else None
 
 
-def up_to_date():
+def up_to_date(out=OUT, defines=()):
     """Rebuild unless the in-tree library was built from exactly these sources."""
-    if not os.path.exists(OUT):
+    if not os.path.exists(out):
         return False
-    stamp = OUT + ".src"
-    return os.path.exists(stamp) and open(stamp).read().strip() == source_hash()
+    stamp = out + ".src"
+    return os.path.exists(stamp) and open(stamp).read().strip() == source_hash(defines)
+
+
+def _cmd(out, defines):
+    digest = source_hash(defines)
+    return digest, [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                    "-munsafe-fp-atomics", "-Wno-unused-result", "-Wl,-Bsymbolic",
+                    *[f"-D{d}" for d in defines], f'-DZV_SRC_HASH="{digest}"', "-o", out + ".tmp",
+                    SRC]
 
 
 def build(force=False, verbose=True, out=None, defines=()):
-    if out is None and not force and up_to_date():
-        return OUT
-    out = out or OUT
-    digest = source_hash(defines)
-    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-munsafe-fp-atomics", "-Wno-unused-result", *[f"-D{d}" for d in defines],
-           f'-DZV_SRC_HASH="{digest}"', "-o", out + ".tmp", SRC]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.check_call(cmd)
-    os.replace(out + ".tmp", out)
-    with open(out + ".src", "w") as f:
-        f.write(digest + "\n")
-    return out
+    """Build the engine libraries (both operand formats, compiled in parallel); with `out`,
+    one alternative build (A/B runs)."""
+    jobs = [(out, tuple(defines))] if out else list(VARIANTS)
+    jobs = [(o, d) for o, d in jobs if force or out or not up_to_date(o, d)]
+    procs = []
+    for o, d in jobs:
+        digest, cmd = _cmd(o, d)
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append((o, digest, subprocess.Popen(cmd)))
+    for o, digest, pr in procs:
+        if pr.wait() != 0:
+            raise subprocess.CalledProcessError(pr.returncode, "hipcc " + o)
+        os.replace(o + ".tmp", o)
+        with open(o + ".src", "w") as f:
+            f.write(digest + "\n")
+    return out or OUT
 
 
 if __name__ == "__main__":

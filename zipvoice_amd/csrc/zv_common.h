@@ -9,10 +9,26 @@
 #include <type_traits>
 #include <utility>
 
+// The 16-bit MFMA operand element.  `bf16` is bf16 in the default build; the fp16-operand
+// build of the same sources (-DZV_OPERAND_F16, libzipvoice_hip_f16.so) makes it IEEE fp16:
+// 11 significant bits instead of 8 at the same MFMA rate on gfx950 (v_mfma_f32_16x16x32_f16),
+// the operand format of the parity-grade fast mode.  Every producer writes
+// its GEMM operands through (bf16) casts (round to nearest even in either format).
+#ifdef ZV_OPERAND_F16
+typedef _Float16 bf16;
+typedef _Float16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 bf16x2 __attribute__((ext_vector_type(2)));
+#define ZV_MFMA_16x16x32 __builtin_amdgcn_mfma_f32_16x16x32_f16
+#define ZV_OPERAND_NAME "fp16"
+#else
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+#define ZV_MFMA_16x16x32 __builtin_amdgcn_mfma_f32_16x16x32_bf16
+#define ZV_OPERAND_NAME "bf16"
+#endif
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define ZV_CHECK(expr)                                                                  \

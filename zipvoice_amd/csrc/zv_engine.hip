@@ -160,7 +160,7 @@ struct zv_engine {
   // one tile per block (gridx -1), the others persistent over the resident grid (0).
   int occ_plain = 2, occ_resid = 2, occ_fused = 2;
   int gridx_plain = 0, gridx_resid = -1, gridx_fused = 0;
-  int gemm_pp = 1;                 // ZV_GEMM_PP: bf16 linears with N % 128 == 0 (and the GLU / NA
+  int gemm_pp = 0;                 // ZV_GEMM_PP: bf16 linears with N % 128 == 0 (and the GLU / NA
                                    // in-projections) on the ping-pong kernel (zv_gemm_pp.inc);
                                    // 0 = the 128x128 kernels (A/B arm, bitwise equal)
   int resid_ws = 1;                // residual linears on the wave-specialised epilogue kernel:
@@ -208,7 +208,7 @@ struct zv_engine {
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
     resid_ws = envi("ZV_RESID_WS", 1);
-    gemm_pp = envi("ZV_GEMM_PP", 1);
+    gemm_pp = envi("ZV_GEMM_PP", 0);
   }
   // ---------------------------------------------------------------- HIP graphs
   // The whole N-step Euler solve (~250 launches per step) is captured once per
@@ -237,6 +237,7 @@ struct zv_engine {
   hipEvent_t gev_in = nullptr, gev_out = nullptr;
   DBuf gx, gtc, gsc, gpad, ggrows;
   bool graphs_enabled = true;
+  bool io_split = false;           // set per decoder call: ZV_MIXED's split in/out projections
 
   void drop_graphs() {
     for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
@@ -794,8 +795,15 @@ struct zv_engine {
     const int D = Z.dim;
     const bool split = SPLIT == 3;
     float* main = ws.main.get<float>(M * D);
-    Act main_a = ws.main_a.get(M, D, split || (SPLIT == 1 && pair_resid));
-    { Out o; o.C = main; o.ldc = D; linear<SPLIT>(Z.in_proj[sidx], xin, M, o, s); }
+    // mixed mode: the input / output projections as split products (xin and the last
+    // BiasNorm's copy main_a carry the lo halves)
+    const bool ios = SPLIT == 1 && io_split;
+    Act main_a = ws.main_a.get(M, D, split || ios || (SPLIT == 1 && pair_resid));
+    {
+      Out o; o.C = main; o.ldc = D;
+      if (ios) linear<3>(Z.in_proj[sidx], xin, M, o, s);
+      else linear<SPLIT>(Z.in_proj[sidx], xin, M, o, s);
+    }
     // time embedding MLP (zipformer.py:267-278) + per-stack projections (:726-729)
     float* tstack = nullptr;
     if (Z.has_time) {
@@ -845,13 +853,17 @@ struct zv_engine {
     }
     // factors end with 1: the last stack's final BiasNorm wrote main_a
     ZV_REQUIRE(Z.stacks.back().ds == 1, "last stack must have downsampling factor 1");
-    { Out o; o.C = out; o.ldc = Z.out_proj[sidx].N; linear<SPLIT>(Z.out_proj[sidx], main_a, M, o, s); }
+    {
+      Out o; o.C = out; o.ldc = Z.out_proj[sidx].N;
+      if (ios) linear<3>(Z.out_proj[sidx], main_a, M, o, s);
+      else linear<SPLIT>(Z.out_proj[sidx], main_a, M, o, s);
+    }
   }
 
   Act build_xin(Workspace& ws, const float* x, const float* tc, const float* sc, int B, int T,
                 int Fx, int copies, int zero_speech, hipStream_t s) {
     const int Ft = cfg.feat_dim, Fin = 2 * Fx + Ft;
-    const bool split = cfg.precision == ZV_FP32;
+    const bool split = cfg.precision != ZV_BF16;     // fp32 / mixed: split input projection
     const long N = (long)copies * B;
     Act xin = ws.xin.get(N * T, round_up(Fin, 64), split);
     hipLaunchKernelGGL(zv_build_input_kernel, grid1d(N * T * Fin), dim3(256), 0, s, x, tc, sc,
@@ -865,6 +877,7 @@ struct zv_engine {
     int sidx = 0;
     if (stereo()) sidx = (Fin == dec.in_proj[0].K) ? 0 : 1;
     ZV_REQUIRE(Fin == dec.in_proj[sidx].K, "decoder input width does not match in_proj");
+    io_split = cfg.precision == ZV_MIXED;
     if (cfg.precision == ZV_FP32) zipformer<3>(dec, ws_dec, xin, sidx, N, T, pad, t, g, out, s);
     else zipformer<1>(dec, ws_dec, xin, sidx, N, T, pad, t, g, out, s);
   }
@@ -1018,7 +1031,8 @@ struct zv_engine {
                    float* out, hipStream_t s) {
     const long n = (long)B * S;
     const int E = cfg.text_embed_dim;
-    const bool split = cfg.precision == ZV_FP32;
+    const bool split = cfg.precision != ZV_BF16;     // mixed: the text encoder is split too
+    io_split = false;
     Act emb = ws_txt.emb.get(n, round_up(E, 64), split);
     hipLaunchKernelGGL(zv_embed_kernel, grid1d(n * E), dim3(256), 0, s, tok, embed_table, emb.h,
                        emb.l, emb.ld, n, E);
@@ -1119,14 +1133,17 @@ const char* zv_last_error(void) { return g_last_error.c_str(); }
 #ifndef ZV_SRC_HASH
 #define ZV_SRC_HASH "unknown"
 #endif
-const char* zv_version(void) { return "zipvoice_hip 0.2 (gfx950) src=" ZV_SRC_HASH; }
+const char* zv_version(void) {
+  return "zipvoice_hip 0.2 (gfx950, " ZV_OPERAND_NAME " operands) src=" ZV_SRC_HASH;
+}
 
 zv_handle zv_create(const zv_config* cfg) {
   try {
     ZV_REQUIRE(cfg != nullptr, "null config");
     ZV_REQUIRE(cfg->num_stacks >= 1 && cfg->num_stacks <= ZV_MAX_STACKS, "bad num_stacks");
     ZV_REQUIRE(cfg->variant >= 0 && cfg->variant <= 3, "bad variant");
-    ZV_REQUIRE(cfg->precision == ZV_FP32 || cfg->precision == ZV_BF16, "bad precision");
+    ZV_REQUIRE(cfg->precision == ZV_FP32 || cfg->precision == ZV_BF16 || cfg->precision == ZV_MIXED,
+               "bad precision");
     return new zv_engine(*cfg);
   } catch (const std::exception& e) {
     g_last_error = e.what();

@@ -20,10 +20,17 @@ from .weights import check_state_dict
 
 LIB_NAME = "libzipvoice_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# the same engine built with IEEE fp16 MFMA operands (csrc/build.py VARIANTS)
+LIB_F16_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libzipvoice_hip_f16.so")
 MAX_STACKS = 8
 VARIANT_ID = {"zipvoice": 0, "zipvoice_distill": 1, "zipvoice_dialog": 2,
               "zipvoice_dialog_stereo": 3}
-PRECISION_ID = {"fp32": 0, "bf16": 1}
+PRECISION_ID = {"fp32": 0, "bf16": 1}      # vocoder / BigVGAN precisions (main library)
+# decoder precision modes: name -> (library, zv_precision).  "fp16" is the parity-grade fast
+# mode: fp16 MFMA operands in the decoder layers, split products for the decoder's input /
+# output projections and the text encoder (ZV_MIXED in the fp16 library)
+MODES = {"fp32": ("bf16", 0), "bf16": ("bf16", 1), "fp16": ("f16", 2),
+         "fp16_plain": ("f16", 1), "bf16_mixed": ("bf16", 2)}
 
 
 class ZvConfig(ctypes.Structure):
@@ -91,35 +98,41 @@ SIGNATURES = {
     "zv_fbank_configure": (_I, [_P, _I, _F, _F]),
 }
 
-_lib = None
+_libs: Dict[str, ctypes.CDLL] = {}
+_lib = None            # the main (bf16-operand) library
 
 
-def load_library(path: Optional[str] = None):
-    """dlopen the engine (fails loudly when it has not been built).  ZV_LIB_PATH
-    selects an alternative build of the same library (A/B measurements)."""
+def load_library(path: Optional[str] = None, operand: str = "bf16"):
+    """dlopen the engine (fails loudly when it has not been built).  operand "f16" loads the
+    fp16-operand build.  ZV_LIB_PATH selects an alternative build of the main library (A/B
+    measurements).  Both are loaded RTLD_LOCAL (and linked -Bsymbolic): the two libraries
+    export the same entry points and each binds its own."""
     global _lib
-    if _lib is not None:
-        return _lib
-    path = path or os.environ.get("ZV_LIB_PATH") or LIB_PATH
+    if path is None:
+        path = LIB_F16_PATH if operand == "f16" else (os.environ.get("ZV_LIB_PATH") or LIB_PATH)
+    if path in _libs:
+        return _libs[path]
     if not os.path.exists(path):
         raise RuntimeError(
-            f"{LIB_NAME} not found at {path}: build it with "
+            f"{os.path.basename(path)} not found at {path}: build it with "
             "`python zipvoice_amd/csrc/build.py` (or __graft_entry__.build()). "
             "There is no CPU fallback for the ZipVoice hot path.")
-    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
     for name, (res, args) in SIGNATURES.items():
-        if path != LIB_PATH and not hasattr(lib, name):
+        if path not in (LIB_PATH, LIB_F16_PATH) and not hasattr(lib, name):
             continue        # an older A/B build without this entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
+    _libs[path] = lib
+    if operand != "f16" and _lib is None:
+        _lib = lib
     return lib
 
 
-def _check(rc: int):
+def _check(rc: int, lib=None):
     if rc != 0:
-        msg = _lib.zv_last_error().decode()
+        msg = (lib or _lib).zv_last_error().decode()
         if "missing weight" in msg or "expected" in msg or "unexpected" in msg:
             raise KeyError(msg)
         raise RuntimeError(f"zipvoice_hip: {msg}")
@@ -128,7 +141,7 @@ def _check(rc: int):
 def make_zv_config(cfg: ModelConfig, precision: str) -> ZvConfig:
     c = ZvConfig()
     c.variant = VARIANT_ID[cfg.variant]
-    c.precision = PRECISION_ID[precision]
+    c.precision = MODES[precision][1]
     c.feat_dim = cfg.feat_dim
     n = len(cfg.fm_decoder_downsampling_factor)
     if n > MAX_STACKS:
@@ -148,18 +161,28 @@ def make_zv_config(cfg: ModelConfig, precision: str) -> ZvConfig:
 
 
 def profile(enable: bool, detail: bool = False):
-    """Enable/disable (and clear) the engine's per-launch event profiler;
-    ``detail`` keys the GEMM records by shape."""
-    lib = load_library()
-    _check(lib.zv_profile((2 if detail else 1) if enable else 0))
+    """Enable/disable (and clear) the engine's per-launch event profiler (in every loaded
+    engine library); ``detail`` keys the GEMM records by shape."""
+    load_library()
+    for lib in list(_libs.values()):
+        _check(lib.zv_profile((2 if detail else 1) if enable else 0), lib)
 
 
 def profile_report() -> dict:
+    """{tag: {launches, flops, bytes, ms}} merged over the loaded engine libraries."""
     import json
-    lib = load_library()
-    buf = ctypes.create_string_buffer(1 << 20)
-    _check(lib.zv_profile_report(buf, len(buf)))
-    return json.loads(buf.value.decode())
+    load_library()
+    rep: dict = {}
+    for lib in list(_libs.values()):
+        buf = ctypes.create_string_buffer(1 << 20)
+        _check(lib.zv_profile_report(buf, len(buf)), lib)
+        for k, v in json.loads(buf.value.decode()).items():
+            if k in rep:
+                for f in ("launches", "flops", "bytes", "ms"):
+                    rep[k][f] += v[f]
+            else:
+                rep[k] = v
+    return rep
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -175,11 +198,13 @@ class HipEngine:
 
     def __init__(self, cfg: ModelConfig, state_dict: Dict[str, np.ndarray],
                  precision: str = "fp32", device: Optional[torch.device] = None):
-        if precision not in PRECISION_ID:
-            raise ValueError(f"precision must be one of {list(PRECISION_ID)}")
+        if precision not in MODES:
+            raise ValueError(f"precision must be one of {list(MODES)}")
         if not torch.cuda.is_available():
             raise RuntimeError("zipvoice_amd needs a ROCm GPU (MI355X); no CPU fallback exists")
-        self.lib = load_library()
+        operand, self.mode_id = MODES[precision]
+        load_library()                       # the main library (error strings, profiler)
+        self.lib = load_library(operand=operand)
         self.cfg = cfg
         self.precision = precision
         self.device = torch.device(device if device is not None else "cuda")
@@ -193,9 +218,9 @@ class HipEngine:
                 raise RuntimeError(self.lib.zv_last_error().decode())
             for k, v in state_dict.items():
                 a = np.ascontiguousarray(np.asarray(v, dtype=np.float32))
-                _check(self.lib.zv_set_weight(self.h, k.encode(), a.ctypes.data_as(ctypes.c_void_p),
+                self._check(self.lib.zv_set_weight(self.h, k.encode(), a.ctypes.data_as(ctypes.c_void_p),
                                               a.size))
-            _check(self.lib.zv_finalize(self.h))
+            self._check(self.lib.zv_finalize(self.h))
 
     def __del__(self):
         h = getattr(self, "h", None)
@@ -206,6 +231,9 @@ class HipEngine:
                 pass
             self.lib.zv_destroy(h)
             self.h = None
+
+    def _check(self, rc: int):
+        _check(rc, self.lib)
 
     # ------------------------------------------------------------------ checks
     def _f32(self, t: torch.Tensor, name: str, shape=None) -> torch.Tensor:
@@ -248,7 +276,7 @@ class HipEngine:
         else:
             out_w = self.cfg.feat_dim
         v = torch.empty((N, T, out_w), dtype=torch.float32, device=self.device)
-        _check(self.lib.zv_fm_decoder(self.h, _ptr(t), _ptr(g), _ptr(xt), _ptr(text_c),
+        self._check(self.lib.zv_fm_decoder(self.h, _ptr(t), _ptr(g), _ptr(xt), _ptr(text_c),
                                       _ptr(speech_c), _ptr(pm), N, T, Fx, _ptr(v), _stream()))
         return v
 
@@ -272,10 +300,10 @@ class HipEngine:
         v = torch.empty_like(x)
         gr = self._guidance_rows(guidance_scale, B)
         if gr is not None:
-            _check(self.lib.zv_velocity_rows(self.h, float(t), _ptr(gr), _ptr(x), _ptr(text_c),
+            self._check(self.lib.zv_velocity_rows(self.h, float(t), _ptr(gr), _ptr(x), _ptr(text_c),
                                              _ptr(speech_c), _ptr(pm), B, T, _ptr(v), _stream()))
         else:
-            _check(self.lib.zv_velocity(self.h, float(t), float(guidance_scale), _ptr(x),
+            self._check(self.lib.zv_velocity(self.h, float(t), float(guidance_scale), _ptr(x),
                                         _ptr(text_c), _ptr(speech_c), _ptr(pm), B, T, _ptr(v),
                                         _stream()))
         return v
@@ -289,12 +317,12 @@ class HipEngine:
         pm = self._mask(padding_mask, (B, T))
         gr = self._guidance_rows(guidance_scale, B)
         if gr is not None:
-            _check(self.lib.zv_euler_sample_rows(self.h, _ptr(x), _ptr(text_c), _ptr(speech_c),
+            self._check(self.lib.zv_euler_sample_rows(self.h, _ptr(x), _ptr(text_c), _ptr(speech_c),
                                                  _ptr(pm), B, T, int(num_step), _ptr(gr),
                                                  float(t_start), float(t_end), float(t_shift),
                                                  _stream()))
         else:
-            _check(self.lib.zv_euler_sample(self.h, _ptr(x), _ptr(text_c), _ptr(speech_c),
+            self._check(self.lib.zv_euler_sample(self.h, _ptr(x), _ptr(text_c), _ptr(speech_c),
                                             _ptr(pm), B, T, int(num_step), float(guidance_scale),
                                             float(t_start), float(t_end), float(t_shift),
                                             _stream()))
@@ -302,7 +330,7 @@ class HipEngine:
 
     def reserve(self, max_batch: int, max_frames: int) -> None:
         """Pre-size the decoder workspace (zv_reserve)."""
-        _check(self.lib.zv_reserve(self.h, int(max_batch), int(max_frames)))
+        self._check(self.lib.zv_reserve(self.h, int(max_batch), int(max_frames)))
 
     def text_encode(self, tokens: torch.Tensor, padding_mask: torch.Tensor,
                     spk: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -312,7 +340,7 @@ class HipEngine:
         if spk is not None:
             spk = spk.to(self.device, torch.int8).contiguous()
         out = torch.empty((B, S, self.cfg.feat_dim), dtype=torch.float32, device=self.device)
-        _check(self.lib.zv_text_encode(self.h, _ptr(tokens), _ptr(pm), _ptr(spk), B, S, _ptr(out),
+        self._check(self.lib.zv_text_encode(self.h, _ptr(tokens), _ptr(pm), _ptr(spk), B, S, _ptr(out),
                                        _stream()))
         return out
 
@@ -322,7 +350,7 @@ class HipEngine:
         tl = tokens_lens.to(self.device, torch.int32).contiguous()
         fl = features_lens.to(self.device, torch.int32).contiguous()
         out = torch.empty((B, num_frames, C), dtype=torch.float32, device=self.device)
-        _check(self.lib.zv_text_condition(self.h, _ptr(embed), B, S, _ptr(tl), _ptr(fl),
+        self._check(self.lib.zv_text_condition(self.h, _ptr(embed), B, S, _ptr(tl), _ptr(fl),
                                           int(num_frames), _ptr(out), _stream()))
         return out
 
@@ -331,6 +359,6 @@ class HipEngine:
         pf = self._f32(prompt_features, "prompt_features")
         pl = prompt_lens.to(self.device, torch.int32).contiguous()
         out = torch.empty((B, num_frames, F), dtype=torch.float32, device=self.device)
-        _check(self.lib.zv_speech_condition(self.h, _ptr(pf), B, Tp, F, _ptr(pl), int(num_frames),
+        self._check(self.lib.zv_speech_condition(self.h, _ptr(pf), B, Tp, F, _ptr(pl), int(num_frames),
                                             _ptr(out), _stream()))
         return out
