@@ -334,7 +334,8 @@ def main():
                 "value": round(frames / (ms16 * 1e-3), 1), "unit": "mel-frames/s",
                 "vs_bf16_time": round(ms16 / ms, 3),
                 "note": "fp16 MFMA operands in the decoder layers, split products for the "
-                        "decoder in/out projections and the text encoder: meets the north-star "
+                        "decoder in/out projections, the attention-score projections and the "
+                        "text encoder: meets the north-star "
                         "1e-3 mean |err| bar (tests/test_gpu_parity.py, test_gpu_fullsize.py); "
                         "timed after 2 warm-up steps"}
             del job16, m16

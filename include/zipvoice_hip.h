@@ -53,8 +53,9 @@ enum zv_variant { ZV_ZIPVOICE = 0, ZV_DISTILL = 1, ZV_DIALOG = 2, ZV_DIALOG_STER
  *          operands, fp32 everything else);
  * ZV_BF16: 16-bit MFMA operands, fp32 accumulation / residual stream / softmax;
  * ZV_MIXED: ZV_BF16 for the decoder layers, the split products for the decoder's input /
- *          output projections and the whole text encoder (the cheap linears that carry most
- *          of the 16-bit rounding error into the output).
+ *          output projections, the layers' attention-score projections and the whole text
+ *          encoder (the cheap linears that carry most of the 16-bit rounding error into the
+ *          output).
  * The 16-bit operand format is the library's: bf16 in libzipvoice_hip.so, IEEE fp16 in
  * libzipvoice_hip_f16.so (same entry points, built from the same sources with
  * -DZV_OPERAND_F16).  ZV_MIXED in the fp16 library is the parity-grade fast mode. */

@@ -5,7 +5,8 @@ Tolerances (written here, per north_star "within 1e-3 mel L1"):
   * precision="fp32" (bf16x3 split-product GEMMs, fp32 elsewhere): mean |err|
     < 1e-3 against the reference outputs, max |err| < 3e-2.
   * precision="fp16" (the parity-grade fast mode: fp16 MFMA operands in the decoder
-    layers, split products for the decoder's in/out projections and the text encoder):
+    layers, split products for the decoder's in/out projections, the attention-score
+    projections and the text encoder):
     mean |err| < 1e-3 (the north-star bar), max |err| < 2e-2.
   * precision="bf16" (bf16 MFMA operands, fp32 accumulate/residual/softmax):
     production mode; the reference's own bf16-autocast drift is 1.4e-2 mean

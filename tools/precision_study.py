@@ -204,11 +204,13 @@ def main():
     if "--mixed" in sys.argv:
         arms = []
         base = {g: "fp16" for g in fams}
-        for keep in (["io"], ["io", "attn"], ["io", "qk"], ["io", "attn", "qk"], ["io", "sa"]):
-            for tx in (False, True):
+        for keep in (["io"], ["io", "attn"], ["io", "qk"], ["io", "attn", "qk"], ["io", "sa"],
+                     ["io", "na"], ["io", "attn", "sa"]):
+            for tx in ((False, True) if args.fixture == "sample_c1.npz" else (True,)):
                 arms.append((f"{'+'.join(keep)} fp32, rest fp16{' +text fp32' if tx else ''}",
                              dict(base, **{g: None for g in keep}), tx))
-        run_arms(o, d, arms, args.out.replace(".txt", "_mixed.txt"))
+        run_arms(o, d, arms, args.out.replace(".txt", "_mixed.txt" if args.fixture == "sample_c1.npz"
+                                              else "_mixed_" + args.fixture.replace(".npz", ".txt")))
         return
     arms = [("fp32 (emulation off)", {})]
     arms.append(("all bf16", {f: "bf16" for f in fams}))

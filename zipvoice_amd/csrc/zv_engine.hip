@@ -238,6 +238,7 @@ struct zv_engine {
   DBuf gx, gtc, gsc, gpad, ggrows;
   bool graphs_enabled = true;
   bool io_split = false;           // set per decoder call: ZV_MIXED's split in/out projections
+                                   // and attention-score projections
 
   void drop_graphs() {
     for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
@@ -617,7 +618,13 @@ struct zv_engine {
     // attention weights from the layer input (zipformer.py:526)
     const int qkpN = W.attn_in.N;
     Act qkp = ws.qkp.get(M, qkpN, split);
-    { Out o; o.act = qkp; linear<SPLIT>(W.attn_in, src_a, M, o, s); }
+    {
+      // mixed mode: the attention-score projection as a split product (the layer input
+      // src_a carries its lo half); q, k, p stay 16-bit
+      Out o; o.act = qkp;
+      if (SPLIT == 1 && io_split) linear<3>(W.attn_in, src_a, M, o, s);
+      else linear<SPLIT>(W.attn_in, src_a, M, o, s);
+    }
     // attention: either materialise W (reference structure; A/B path, and the
     // fallback for lengths whose fused LDS images do not fit) or keep only
     // per-row softmax statistics and recompute scores inside each consumer
@@ -834,7 +841,7 @@ struct zv_engine {
       } else {
         const int dL = (T + S.ds - 1) / S.ds;
         float* d = ws.dsrc.get<float>((size_t)N * dL * D);
-        Act d_a = ws.dsrc_a.get((long)N * dL, D, split || (SPLIT == 1 && pair_resid));
+        Act d_a = ws.dsrc_a.get((long)N * dL, D, split || ios || (SPLIT == 1 && pair_resid));
         hipLaunchKernelGGL(zv_downsample_kernel, grid1d((long)N * dL * D), dim3(256), 0, s, main, d,
                            N, T, dL, D, S.ds, S.ds_w);
         ZV_LAUNCH_CHECK();
@@ -1097,13 +1104,13 @@ static float bench_variant(GemmParams p, int iters, bool persistent, hipStream_t
   return ms / iters;
 }
 
-template <int BM, int BN, int WGM, int WGN, int EPI>
+template <int BM, int BN, int WGM, int WGN, int EPI, int STAGES = 2>
 static float bench_variant_pp(GemmParams p, int iters, hipStream_t s) {
   hipEvent_t e0, e1;
   ZV_CHECK(hipEventCreate(&e0)); ZV_CHECK(hipEventCreate(&e1));
-  launch_gemm_pp<BM, BN, WGM, WGN, EPI, 0>(p, s, "bench");
+  launch_gemm_pp<BM, BN, WGM, WGN, EPI, 0, STAGES>(p, s, "bench");
   ZV_CHECK(hipEventRecord(e0, s));
-  for (int i = 0; i < iters; ++i) launch_gemm_pp<BM, BN, WGM, WGN, EPI, 0>(p, s, "bench");
+  for (int i = 0; i < iters; ++i) launch_gemm_pp<BM, BN, WGM, WGN, EPI, 0, STAGES>(p, s, "bench");
   ZV_CHECK(hipEventRecord(e1, s));
   ZV_CHECK(hipEventSynchronize(e1));
   float ms = 0.f;
@@ -1290,6 +1297,8 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
     case 22: ms = bench_variant8<0, false>(p, iters, s); break;
     case 23: ms = bench_variant8<1, false>(p, iters, s); break;
     case 50: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD>(p, iters, s); break;
+    case 52: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD, 3>(p, iters, s); break;   // out mode 4 only
+    case 53: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD, 4>(p, iters, s); break;   // out mode 4 only
     default: throw std::invalid_argument("unknown variant");
   }
   *ms_out = ms;

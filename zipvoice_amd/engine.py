@@ -28,7 +28,8 @@ VARIANT_ID = {"zipvoice": 0, "zipvoice_distill": 1, "zipvoice_dialog": 2,
 PRECISION_ID = {"fp32": 0, "bf16": 1}      # vocoder / BigVGAN precisions (main library)
 # decoder precision modes: name -> (library, zv_precision).  "fp16" is the parity-grade fast
 # mode: fp16 MFMA operands in the decoder layers, split products for the decoder's input /
-# output projections and the text encoder (ZV_MIXED in the fp16 library)
+# output projections, the attention-score projections and the text encoder (ZV_MIXED in the
+# fp16 library)
 MODES = {"fp32": ("bf16", 0), "bf16": ("bf16", 1), "fp16": ("f16", 2),
          "fp16_plain": ("f16", 1), "bf16_mixed": ("bf16", 2)}
 
