@@ -153,6 +153,11 @@ struct zv_engine {
   float* spk_table = nullptr;     // (2, feat_dim)
   float* temb_freqs = nullptr;    // (time_embed_dim/2)
   Workspace ws_dec, ws_txt;
+  Workspace ws_dec2;               // second row half of the decoder (split_streams)
+  int split_streams = 0;           // ZV_SPLIT_STREAMS: decoder row halves on two streams
+  long split_min_rows = 0;         // ... for N*T >= this many rows (ZV_SPLIT_MIN_ROWS)
+  hipStream_t split_stream = nullptr;
+  hipEvent_t split_fork = nullptr, split_join = nullptr;
 
   bool materialize_attn = false;   // A/B: ZV_ATTN_MATERIALIZE=1 keeps the W-materialising path
   // GEMM launch policy by epilogue class (measured same-box, profiles/r01_gemm_policy_ab.txt):
@@ -209,6 +214,8 @@ struct zv_engine {
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
     resid_ws = envi("ZV_RESID_WS", 1);
     gemm_pp = envi("ZV_GEMM_PP", 0);
+    split_streams = envi("ZV_SPLIT_STREAMS", 0);
+    split_min_rows = envi("ZV_SPLIT_MIN_ROWS", 8192);
   }
   // ---------------------------------------------------------------- HIP graphs
   // The whole N-step Euler solve (~250 launches per step) is captured once per
@@ -257,6 +264,9 @@ struct zv_engine {
     if (gstream) (void)hipStreamDestroy(gstream);
     if (gev_in) (void)hipEventDestroy(gev_in);
     if (gev_out) (void)hipEventDestroy(gev_out);
+    if (split_stream) (void)hipStreamDestroy(split_stream);
+    if (split_fork) (void)hipEventDestroy(split_fork);
+    if (split_join) (void)hipEventDestroy(split_join);
     for (void* p : allocs) (void)hipFree(p);
   }
 
@@ -879,14 +889,43 @@ struct zv_engine {
     return xin;
   }
 
+  void decoder_rows(Workspace& ws, Act xin, int sidx, int N, int T, const uint8_t* pad,
+                    const float* t, const float* g, float* out, hipStream_t s) {
+    if (cfg.precision == ZV_FP32) zipformer<3>(dec, ws, xin, sidx, N, T, pad, t, g, out, s);
+    else zipformer<1>(dec, ws, xin, sidx, N, T, pad, t, g, out, s);
+  }
+
   void decoder(Act xin, int Fin, int N, int T, const uint8_t* pad, const float* t, const float* g,
                float* out, hipStream_t s) {
     int sidx = 0;
     if (stereo()) sidx = (Fin == dec.in_proj[0].K) ? 0 : 1;
     ZV_REQUIRE(Fin == dec.in_proj[sidx].K, "decoder input width does not match in_proj");
     io_split = cfg.precision == ZV_MIXED;
-    if (cfg.precision == ZV_FP32) zipformer<3>(dec, ws_dec, xin, sidx, N, T, pad, t, g, out, s);
-    else zipformer<1>(dec, ws_dec, xin, sidx, N, T, pad, t, g, out, s);
+    if (!split_streams || N < 2 || (long)N * T < split_min_rows) {
+      decoder_rows(ws_dec, xin, sidx, N, T, pad, t, g, out, s);
+      return;
+    }
+    // Two independent row halves on two streams (rows never interact on this path): the
+    // kernels of one half (GEMM: MFMA/LDS) co-run with the other half's (attention: VALU,
+    // epilogues: HBM) instead of the whole batch passing each kernel in lock step.
+    if (!split_stream) {
+      ZV_CHECK(hipStreamCreateWithFlags(&split_stream, hipStreamNonBlocking));
+      ZV_CHECK(hipEventCreateWithFlags(&split_fork, hipEventDisableTiming));
+      ZV_CHECK(hipEventCreateWithFlags(&split_join, hipEventDisableTiming));
+    }
+    const int N1 = N / 2, N2 = N - N1;
+    const long r1 = (long)N1 * T;
+    const int outN = dec.out_proj[sidx].N;
+    Act xin2 = xin;
+    xin2.h += r1 * xin.ld;
+    if (xin.l) xin2.l += r1 * xin.ld;
+    ZV_CHECK(hipEventRecord(split_fork, s));
+    ZV_CHECK(hipStreamWaitEvent(split_stream, split_fork, 0));
+    decoder_rows(ws_dec, xin, sidx, N1, T, pad, t, g, out, s);
+    decoder_rows(ws_dec2, xin2, sidx, N2, T, pad ? pad + r1 : nullptr, t + N1, g ? g + N1 : nullptr,
+                 out + r1 * outN, split_stream);
+    ZV_CHECK(hipEventRecord(split_join, split_stream));
+    ZV_CHECK(hipStreamWaitEvent(s, split_join, 0));
   }
 
   // guided velocity at scalar t for B un-doubled rows (solver.py:40-165).
@@ -1397,7 +1436,7 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
 
 int64_t zv_device_bytes(zv_handle h) {
   if (!h) return 0;
-  return (int64_t)(h->weight_bytes + h->ws_dec.bytes() + h->ws_txt.bytes() + h->gx.bytes +
+  return (int64_t)(h->weight_bytes + h->ws_dec.bytes() + h->ws_dec2.bytes() + h->ws_txt.bytes() + h->gx.bytes +
                    h->gtc.bytes + h->gsc.bytes + h->gpad.bytes + h->ggrows.bytes);
 }
 
