@@ -1,0 +1,47 @@
+"""SelfAttention with the positional term as a Toeplitz MFMA product
+(zv_attn_sa_tp_kernel, default in the 16-bit modes) against the VALU form
+(zv_attn_sa_kernel, ZV_SA_TP=0) and the oracle.  The two differ only in where the
+positional table is rounded (16-bit operand vs fp32 FMAs) and the summation order, so
+they agree to the 16-bit mode's own resolution; each stays inside its mode's parity bar
+against the fp32 oracle (bf16: mean 5e-2; fp16 mixed mode, whose table carries a lo half:
+mean 1e-3)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.mark.parametrize("precision,bar,ab", [("bf16", 5e-2, 2e-2), ("fp16", 1e-3, 1e-3)])
+def test_sa_tp_vs_valu_and_oracle(monkeypatch, precision, bar, ab):
+    from oracle.zipvoice_np import ZipVoiceOracle
+    from zipvoice_amd.config import default_config
+    from zipvoice_amd.models import build_model
+    from zipvoice_amd.weights import synthetic_state_dict
+    cfg = default_config("zipvoice")
+    sd = synthetic_state_dict(cfg, 0)
+    rng = np.random.default_rng(11)
+    B, T, lens = 2, 203, [203, 150]
+    x = rng.standard_normal((B, T, 100), dtype=np.float32)
+    tc = rng.standard_normal((B, T, 100), dtype=np.float32)
+    sc = rng.standard_normal((B, T, 100), dtype=np.float32)
+    pm = np.arange(T)[None] >= np.array(lens)[:, None]
+    cu = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0")
+    outs = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("ZV_SA_TP", flag)
+        m = build_model(cfg, precision=precision)
+        m.load_state_dict(sd)
+        m = m.to("cuda:0")
+        outs[flag] = m.engine.velocity(0.4, 1.0, cu(x), cu(tc), cu(sc), cu(pm)).cpu().numpy()
+        del m
+    ref = ZipVoiceOracle(cfg, sd).velocity(np.float32(0.4), x, tc, sc, pm, 1.0)
+    valid = ~pm
+    d_ab = np.abs(outs["0"] - outs["1"])[valid].mean()
+    print(f"{precision}: mean |tp - valu| = {d_ab:.3e}")
+    for flag, o in outs.items():
+        e = np.abs(o - ref)[valid]
+        print(f"{precision} ZV_SA_TP={flag}: vs oracle mean {e.mean():.3e} max {e.max():.3e}")
+        assert e.mean() < bar
+    assert d_ab < ab

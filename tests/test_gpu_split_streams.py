@@ -1,8 +1,8 @@
-"""Decoder row halves on two streams (ZV_SPLIT_STREAMS=1, zv_engine::decoder) against the
-single-stream decoder: rows never interact on the path (every kernel is per row, per
-(row, head) or per output element with a fixed K order), so the velocity, a guided Euler
-solve replayed from its graph, and the per-utterance-guidance / Distill variants must be
-bitwise equal."""
+"""Decoder row blocks on 2-4 streams (ZV_SPLIT_STREAMS, zv_engine::decoder; default 2)
+against the single-stream decoder (ZV_SPLIT_STREAMS=1): rows never interact on the path
+(every kernel is per row, per (row, head) or per output element with a fixed K order), so
+the velocity, a guided Euler solve replayed from its graph, and the per-utterance-guidance
+/ Distill variants must be bitwise equal."""
 import numpy as np
 import pytest
 
@@ -20,9 +20,10 @@ def _inputs(B, T, lens, seed):
     return x, tc, sc, pm
 
 
-@pytest.mark.parametrize("variant,precision", [("zipvoice", "bf16"), ("zipvoice", "fp32"),
-                                               ("zipvoice_distill", "bf16")])
-def test_split_streams_bitwise(monkeypatch, variant, precision):
+@pytest.mark.parametrize("variant,precision,parts", [("zipvoice", "bf16", "2"), ("zipvoice", "fp32", "2"),
+                                                     ("zipvoice_distill", "bf16", "2"),
+                                                     ("zipvoice", "bf16", "3"), ("zipvoice", "fp16", "4")])
+def test_split_streams_bitwise(monkeypatch, variant, precision, parts):
     from zipvoice_amd.config import default_config
     from zipvoice_amd.models import build_model
     from zipvoice_amd.weights import synthetic_state_dict
@@ -32,7 +33,7 @@ def test_split_streams_bitwise(monkeypatch, variant, precision):
     x, tc, sc, pm = _inputs(B, T, [1500, 1200, 777], seed=3)
     g_rows = torch.tensor([1.0, 0.0, 2.0]).reshape(B, 1, 1)
     outs = []
-    for flag in ("0", "1"):
+    for flag in ("1", parts):
         monkeypatch.setenv("ZV_SPLIT_STREAMS", flag)
         monkeypatch.setenv("ZV_SPLIT_MIN_ROWS", "2048")
         m = build_model(cfg, precision=precision)

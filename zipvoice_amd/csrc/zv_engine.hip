@@ -90,6 +90,9 @@ struct DBuf {
       if (p) { ZV_CHECK(hipDeviceSynchronize()); ZV_CHECK(hipFree(p)); }
       ZV_CHECK(hipMalloc(&p, need));
       ZV_CHECK(hipMemset(p, 0, need));
+      // the memset runs on the null stream, which does not order against the engine's
+      // non-blocking streams (graph / split-decoder streams): finish it before any use
+      ZV_CHECK(hipDeviceSynchronize());
       bytes = need;
     }
     return reinterpret_cast<T*>(p);
@@ -153,11 +156,13 @@ struct zv_engine {
   float* spk_table = nullptr;     // (2, feat_dim)
   float* temb_freqs = nullptr;    // (time_embed_dim/2)
   Workspace ws_dec, ws_txt;
-  Workspace ws_dec2;               // second row half of the decoder (split_streams)
-  int split_streams = 0;           // ZV_SPLIT_STREAMS: decoder row halves on two streams
+  static constexpr int MAX_SPLIT = 4;
+  Workspace ws_split[MAX_SPLIT - 1];   // row blocks 1.. of the split decoder
+  int split_streams = 2;           // ZV_SPLIT_STREAMS: decoder row blocks on this many streams
+                                   // (<= 1: one stream; bench A/B: profiles/r02_split_ab.txt)
   long split_min_rows = 0;         // ... for N*T >= this many rows (ZV_SPLIT_MIN_ROWS)
-  hipStream_t split_stream = nullptr;
-  hipEvent_t split_fork = nullptr, split_join = nullptr;
+  hipStream_t split_stream[MAX_SPLIT - 1] = {};
+  hipEvent_t split_fork = nullptr, split_join[MAX_SPLIT - 1] = {};
 
   bool materialize_attn = false;   // A/B: ZV_ATTN_MATERIALIZE=1 keeps the W-materialising path
   // GEMM launch policy by epilogue class (measured same-box, profiles/r01_gemm_policy_ab.txt):
@@ -170,6 +175,8 @@ struct zv_engine {
                                    // 0 = the 128x128 kernels (A/B arm, bitwise equal)
   int resid_ws = 1;                // residual linears on the wave-specialised epilogue kernel:
                                    // ZV_RESID_WS 1 = K <= 64 only (default), 2 = all, 0 = none
+  int sa_tp = 1;                   // ZV_SA_TP: 16-bit modes' SelfAttention with the positional
+                                   // term on the MFMA chain (zv_attn_sa_tp_kernel); 0 = VALU form
   bool sa_pos_mfma = false;        // A/B: ZV_SA_POS_MFMA=1 puts the SelfAttention positional term on
                                    // f32 MFMA (parity-green, same time: the loop is latency bound)
   bool skinny_tiles = true;        // V^T projection (N = 48) on 64x64 tiles, one per block
@@ -209,12 +216,13 @@ struct zv_engine {
     gridx_fused = envi("ZV_GEMM_GRIDX_FUSED", 0);
     fused_tile = envi("ZV_GEMM_FUSED_TILE", 0);
     sa_pos_mfma = envi("ZV_SA_POS_MFMA", 0) != 0;
+    sa_tp = envi("ZV_SA_TP", 1);
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
     resid_ws = envi("ZV_RESID_WS", 1);
     gemm_pp = envi("ZV_GEMM_PP", 0);
-    split_streams = envi("ZV_SPLIT_STREAMS", 0);
+    split_streams = envi("ZV_SPLIT_STREAMS", 2);
     split_min_rows = envi("ZV_SPLIT_MIN_ROWS", 8192);
   }
   // ---------------------------------------------------------------- HIP graphs
@@ -264,9 +272,11 @@ struct zv_engine {
     if (gstream) (void)hipStreamDestroy(gstream);
     if (gev_in) (void)hipEventDestroy(gev_in);
     if (gev_out) (void)hipEventDestroy(gev_out);
-    if (split_stream) (void)hipStreamDestroy(split_stream);
+    for (int i = 0; i < MAX_SPLIT - 1; ++i) {
+      if (split_stream[i]) (void)hipStreamDestroy(split_stream[i]);
+      if (split_join[i]) (void)hipEventDestroy(split_join[i]);
+    }
     if (split_fork) (void)hipEventDestroy(split_fork);
-    if (split_join) (void)hipEventDestroy(split_join);
     for (void* p : allocs) (void)hipFree(p);
   }
 
@@ -725,7 +735,15 @@ struct zv_engine {
         f.vh = vt.h; f.vl = vt.l; f.ldv = Lpad; f.sv_b = (long)HV * Lpad; f.vrows_per_head = vd;
         f.nv = vd;
         f.oh = o.h; f.ol = o.l; f.ldo = o.ld; f.ocol_per_head = vd;
-        if (sa_pos_mfma) launch_attn_sa_mf<SPLIT>(f, s);
+        bool done = false;
+        if constexpr (SPLIT == 1)
+          if (sa_tp && !sa_pos_mfma) {   // positional term as a Toeplitz MFMA product
+            if (io_split) launch_attn_sa_tp<1>(f, s);
+            else launch_attn_sa_tp<0>(f, s);
+            done = true;
+          }
+        if (done) {}
+        else if (sa_pos_mfma) launch_attn_sa_mf<SPLIT>(f, s);
         else launch_attn_sa<SPLIT>(f, s);
       }
       Out e = res;
@@ -901,31 +919,42 @@ struct zv_engine {
     if (stereo()) sidx = (Fin == dec.in_proj[0].K) ? 0 : 1;
     ZV_REQUIRE(Fin == dec.in_proj[sidx].K, "decoder input width does not match in_proj");
     io_split = cfg.precision == ZV_MIXED;
-    if (!split_streams || N < 2 || (long)N * T < split_min_rows) {
+    // (profiled passes run one stream: per-kernel event durations stay per-kernel)
+    if (split_streams < 2 || N < 2 || (long)N * T < split_min_rows || g_zv_prof.on) {
       decoder_rows(ws_dec, xin, sidx, N, T, pad, t, g, out, s);
       return;
     }
-    // Two independent row halves on two streams (rows never interact on this path): the
-    // kernels of one half (GEMM: MFMA/LDS) co-run with the other half's (attention: VALU,
+    // Independent row blocks on their own streams (rows never interact on this path): the
+    // kernels of one block (GEMMs: MFMA/LDS) co-run with another block's (attention: VALU;
     // epilogues: HBM) instead of the whole batch passing each kernel in lock step.
-    if (!split_stream) {
-      ZV_CHECK(hipStreamCreateWithFlags(&split_stream, hipStreamNonBlocking));
+    // Bitwise equal to the single-stream decoder (tests/test_gpu_split_streams.py).
+    const int parts = std::min(split_streams, std::min(N, MAX_SPLIT));
+    if (!split_fork) {
       ZV_CHECK(hipEventCreateWithFlags(&split_fork, hipEventDisableTiming));
-      ZV_CHECK(hipEventCreateWithFlags(&split_join, hipEventDisableTiming));
+      for (int i = 0; i < MAX_SPLIT - 1; ++i) {
+        ZV_CHECK(hipStreamCreateWithFlags(&split_stream[i], hipStreamNonBlocking));
+        ZV_CHECK(hipEventCreateWithFlags(&split_join[i], hipEventDisableTiming));
+      }
     }
-    const int N1 = N / 2, N2 = N - N1;
-    const long r1 = (long)N1 * T;
     const int outN = dec.out_proj[sidx].N;
-    Act xin2 = xin;
-    xin2.h += r1 * xin.ld;
-    if (xin.l) xin2.l += r1 * xin.ld;
     ZV_CHECK(hipEventRecord(split_fork, s));
-    ZV_CHECK(hipStreamWaitEvent(split_stream, split_fork, 0));
-    decoder_rows(ws_dec, xin, sidx, N1, T, pad, t, g, out, s);
-    decoder_rows(ws_dec2, xin2, sidx, N2, T, pad ? pad + r1 : nullptr, t + N1, g ? g + N1 : nullptr,
-                 out + r1 * outN, split_stream);
-    ZV_CHECK(hipEventRecord(split_join, split_stream));
-    ZV_CHECK(hipStreamWaitEvent(s, split_join, 0));
+    int r0 = 0;
+    for (int i = 0; i < parts; ++i) {
+      const int n = N / parts + (i < N % parts ? 1 : 0);
+      const long rows = (long)r0 * T;
+      Act xi = xin;
+      xi.h += rows * xin.ld;
+      if (xin.l) xi.l += rows * xin.ld;
+      hipStream_t si = i == 0 ? s : split_stream[i - 1];
+      if (i > 0) ZV_CHECK(hipStreamWaitEvent(si, split_fork, 0));
+      decoder_rows(i == 0 ? ws_dec : ws_split[i - 1], xi, sidx, n, T, pad ? pad + rows : nullptr,
+                   t + r0, g ? g + r0 : nullptr, out + rows * outN, si);
+      r0 += n;
+    }
+    for (int i = 1; i < parts; ++i) {
+      ZV_CHECK(hipEventRecord(split_join[i - 1], split_stream[i - 1]));
+      ZV_CHECK(hipStreamWaitEvent(s, split_join[i - 1], 0));
+    }
   }
 
   // guided velocity at scalar t for B un-doubled rows (solver.py:40-165).
@@ -1436,7 +1465,8 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
 
 int64_t zv_device_bytes(zv_handle h) {
   if (!h) return 0;
-  return (int64_t)(h->weight_bytes + h->ws_dec.bytes() + h->ws_dec2.bytes() + h->ws_txt.bytes() + h->gx.bytes +
+  return (int64_t)(h->weight_bytes + h->ws_dec.bytes() + h->ws_split[0].bytes() + h->ws_split[1].bytes() +
+                   h->ws_split[2].bytes() + h->ws_txt.bytes() + h->gx.bytes +
                    h->gtc.bytes + h->gsc.bytes + h->gpad.bytes + h->ggrows.bytes);
 }
 
