@@ -158,8 +158,8 @@ struct zv_engine {
   Workspace ws_dec, ws_txt;
   static constexpr int MAX_SPLIT = 4;
   Workspace ws_split[MAX_SPLIT - 1];   // row blocks 1.. of the split decoder
-  int split_streams = 2;           // ZV_SPLIT_STREAMS: decoder row blocks on this many streams
-                                   // (<= 1: one stream; bench A/B: profiles/r02_split_ab.txt)
+  int split_streams = 3;           // ZV_SPLIT_STREAMS: decoder row blocks on this many streams
+                                   // (<= 1: one stream; bench A/B: profiles/r02_split_tp_ab.txt)
   long split_min_rows = 0;         // ... for N*T >= this many rows (ZV_SPLIT_MIN_ROWS)
   hipStream_t split_stream[MAX_SPLIT - 1] = {};
   hipEvent_t split_fork = nullptr, split_join[MAX_SPLIT - 1] = {};
@@ -222,7 +222,7 @@ struct zv_engine {
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
     resid_ws = envi("ZV_RESID_WS", 1);
     gemm_pp = envi("ZV_GEMM_PP", 0);
-    split_streams = envi("ZV_SPLIT_STREAMS", 2);
+    split_streams = envi("ZV_SPLIT_STREAMS", 3);
     split_min_rows = envi("ZV_SPLIT_MIN_ROWS", 8192);
   }
   // ---------------------------------------------------------------- HIP graphs
@@ -645,6 +645,10 @@ struct zv_engine {
       if (SPLIT == 1 && io_split) linear<3>(W.attn_in, src_a, M, o, s);
       else linear<SPLIT>(W.attn_in, src_a, M, o, s);
     }
+    // head-0 scoring of the stats / NonlinAttention pair: Toeplitz MFMA form in bf16 mode
+    // (mixed mode keeps the fp32 positional table there: its lo half would not fit the
+    // NonlinAttention image at dialog lengths)
+    const bool tp_na = SPLIT == 1 && sa_tp && !io_split;
     // attention: either materialise W (reference structure; A/B path, and the
     // fallback for lengths whose fused LDS images do not fit) or keep only
     // per-row softmax statistics and recompute scores inside each consumer
@@ -659,7 +663,10 @@ struct zv_engine {
       fp.qh = qkp.h; fp.ql = qkp.l; fp.ldq = qkpN; fp.P = posP; fp.key_pad = pad;
       fp.stats = ws.stats.get<float2>((size_t)M);     // head 0 only (NonlinAttention)
       fp.B = B; fp.L = L; fp.H = H;
-      launch_attn_stats<SPLIT>(fp, s);
+      if constexpr (SPLIT == 1)
+        if (tp_na) launch_attn_stats<1, 1>(fp, s);
+        else launch_attn_stats<1>(fp, s);
+      else launch_attn_stats<SPLIT>(fp, s);
     }
     Out res;                       // cur = cur + module(cur), with the hi/lo copy
     const bool pairm = SPLIT == 1 && pair_resid;
@@ -707,7 +714,16 @@ struct zv_engine {
         f.mulh = y.h; f.mull = y.l; f.ldmul = y.ld;
         f.oh = nao.h; f.ol = nao.l; f.ldo = nao.ld; f.ocol_per_head = 0;
         constexpr int QTILES = SPLIT == 3 ? 4 : 8;
-        if (hid <= 128) launch_attn_na<SPLIT, 1, QTILES>(f, s);
+        bool done = false;
+        if constexpr (SPLIT == 1)
+          if (tp_na) {
+            if (hid <= 128) launch_attn_na<1, 1, QTILES, 1>(f, s);
+            else if (hid <= 256) launch_attn_na<1, 2, QTILES, 1>(f, s);
+            else launch_attn_na<1, 3, QTILES, 1>(f, s);
+            done = true;
+          }
+        if (done) {}
+        else if (hid <= 128) launch_attn_na<SPLIT, 1, QTILES>(f, s);
         else if (hid <= 256) launch_attn_na<SPLIT, 2, QTILES>(f, s);
         else launch_attn_na<SPLIT, 3, QTILES>(f, s);
       }
