@@ -176,7 +176,9 @@ struct zv_engine {
   int resid_ws = 1;                // residual linears on the wave-specialised epilogue kernel:
                                    // ZV_RESID_WS 1 = K <= 64 only (default), 2 = all, 0 = none
   int sa_tp = 1;                   // ZV_SA_TP: 16-bit modes' SelfAttention with the positional
-                                   // term on the MFMA chain (zv_attn_sa_tp_kernel); 0 = VALU form
+                                   // term on the MFMA chain (zv_attn_sa_tp_kernel), the head-0
+                                   // stats / NonlinAttention scoring too; 0 = VALU forms
+                                   // (3: A/B arm, SA with the one-wave register budget)
   bool sa_pos_mfma = false;        // A/B: ZV_SA_POS_MFMA=1 puts the SelfAttention positional term on
                                    // f32 MFMA (parity-green, same time: the loop is latency bound)
   bool skinny_tiles = true;        // V^T projection (N = 48) on 64x64 tiles, one per block
@@ -754,7 +756,10 @@ struct zv_engine {
         bool done = false;
         if constexpr (SPLIT == 1)
           if (sa_tp && !sa_pos_mfma) {   // positional term as a Toeplitz MFMA product
-            if (io_split) launch_attn_sa_tp<1>(f, s);
+            if (sa_tp == 3) {          // A/B: the compiler's one-wave register budget
+              if (io_split) launch_attn_sa_tp<1, 1>(f, s);
+              else launch_attn_sa_tp<0, 1>(f, s);
+            } else if (io_split) launch_attn_sa_tp<1>(f, s);
             else launch_attn_sa_tp<0>(f, s);
             done = true;
           }
@@ -829,7 +834,7 @@ struct zv_engine {
     // synchronisation, graph-capturable
     const int R = 2 * L - 1, HPD = Z.heads * Z.pd, nl = (int)S.layers.size();
     float* posP = ws.posP.get<float>((size_t)std::max(nl, 1) * R * HPD);
-    hipLaunchKernelGGL(zv_posp_kernel, grid1d((long)nl * R), dim3(256), 0, s, S.pos_w_all, posP,
+    hipLaunchKernelGGL(zv_posp_kernel, dim3((unsigned)cdiv((long)nl * R * HPD, 256L)), dim3(256), 0, s, S.pos_w_all, posP,
                        L, nl, HPD, Z.pos_dim);
     ZV_LAUNCH_CHECK();
     for (size_t li = 0; li < S.layers.size(); ++li)
