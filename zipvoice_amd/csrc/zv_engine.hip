@@ -165,11 +165,13 @@ struct zv_engine {
   hipEvent_t split_fork = nullptr, split_join[MAX_SPLIT - 1] = {};
 
   bool materialize_attn = false;   // A/B: ZV_ATTN_MATERIALIZE=1 keeps the W-materialising path
-  // GEMM launch policy by epilogue class (measured same-box, profiles/r01_gemm_policy_ab.txt):
-  // two 4-wave blocks per CU everywhere (OCC 2); the HBM-bound residual-stream linears
-  // one tile per block (gridx -1), the others persistent over the resident grid (0).
+  // GEMM launch policy by epilogue class: two 4-wave blocks per CU everywhere (OCC 2,
+  // profiles/r01_gemm_policy_ab.txt) and one tile per block (gridx -1): with the decoder
+  // split over streams, dynamically dispatched tiles fill the CUs another stream's kernel
+  // leaves idle; the persistent resident grid (0) measured 2.6 % slower for the plain and
+  // fused-epilogue linears (profiles/r02_launch_policy_ab.txt)
   int occ_plain = 2, occ_resid = 2, occ_fused = 2;
-  int gridx_plain = 0, gridx_resid = -1, gridx_fused = 0;
+  int gridx_plain = -1, gridx_resid = -1, gridx_fused = -1;
   int gemm_pp = 0;                 // ZV_GEMM_PP: bf16 linears with N % 128 == 0 (and the GLU / NA
                                    // in-projections) on the ping-pong kernel (zv_gemm_pp.inc);
                                    // 0 = the 128x128 kernels (A/B arm, bitwise equal)
@@ -213,9 +215,9 @@ struct zv_engine {
     occ_resid = o2 ? atoi(o2) : 2;
     occ_fused = o3 ? atoi(o3) : 2;
     auto envi = [](const char* k, int d) { const char* v = getenv(k); return v ? atoi(v) : d; };
-    gridx_plain = envi("ZV_GEMM_GRIDX_PLAIN", 0);
+    gridx_plain = envi("ZV_GEMM_GRIDX_PLAIN", -1);
     gridx_resid = envi("ZV_GEMM_GRIDX_RESID", -1);
-    gridx_fused = envi("ZV_GEMM_GRIDX_FUSED", 0);
+    gridx_fused = envi("ZV_GEMM_GRIDX_FUSED", -1);
     fused_tile = envi("ZV_GEMM_FUSED_TILE", 0);
     sa_pos_mfma = envi("ZV_SA_POS_MFMA", 0) != 0;
     sa_tp = envi("ZV_SA_TP", 1);
