@@ -19,6 +19,7 @@
 #include "zv_common.h"
 #include "zv_gemm.inc"
 #include "zv_gemm_ws.inc"
+#include "zv_gemm_dual.inc"
 #include "zv_gemm8.inc"
 #include "zv_gemm_pp.inc"
 #include "zv_attn.inc"
@@ -172,6 +173,8 @@ struct zv_engine {
   // fused-epilogue linears (profiles/r02_launch_policy_ab.txt)
   int occ_plain = 2, occ_resid = 2, occ_fused = 2;
   int gridx_plain = -1, gridx_resid = -1, gridx_fused = -1;
+  int gemm_dual = 0;               // ZV_GEMM_DUAL: residual linears (K >= 64) on the dual-group
+                                   // kernel (zv_gemm_dual.inc); bitwise equal, A/B arm
   int gemm_pp = 0;                 // ZV_GEMM_PP: bf16 linears with N % 128 == 0 (and the GLU / NA
                                    // in-projections) on the ping-pong kernel (zv_gemm_pp.inc);
                                    // 0 = the 128x128 kernels (A/B arm, bitwise equal)
@@ -226,6 +229,7 @@ struct zv_engine {
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
     resid_ws = envi("ZV_RESID_WS", 1);
     gemm_pp = envi("ZV_GEMM_PP", 0);
+    gemm_dual = envi("ZV_GEMM_DUAL", 0);
     split_streams = envi("ZV_SPLIT_STREAMS", 3);
     split_min_rows = envi("ZV_SPLIT_MIN_ROWS", 8192);
   }
@@ -608,6 +612,14 @@ struct zv_engine {
     }
     if (o.resid) {   // residual-stream linear: its own symbol / tag (HBM roofline)
       const char* rtag = SPLIT == 3 ? "gemm_fp32_resid" : "gemm_bf16_resid";
+      if constexpr (SPLIT == 1)
+        if (gemm_dual && !o.act.l && Lw.K >= 64) {
+          GemmParams q = p;
+          if (gemm_dual_ok(q)) {       // two phase-offset tile groups per CU (zv_gemm_dual.inc)
+            launch_gemm_dual(q, s, "gemm_bf16_resid_dual");
+            return;
+          }
+        }
       if constexpr (SPLIT == 1)
         // wave-specialised epilogue (zv_gemm_ws.inc): faster where the linear is all epilogue
         // (K <= 64: SelfAttention out-projections, -8 %); its single 4-wave MMA group per CU
@@ -1390,6 +1402,20 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
     case 50: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD>(p, iters, s); break;
     case 52: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD, 3>(p, iters, s); break;   // out mode 4 only
     case 53: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD, 4>(p, iters, s); break;   // out mode 4 only
+    case 60: {                     // dual-group residual kernel (out mode 2 only)
+      if (out_mode != 2) throw std::invalid_argument("variant 60: residual mode only");
+      hipEvent_t e0, e1;
+      ZV_CHECK(hipEventCreate(&e0)); ZV_CHECK(hipEventCreate(&e1));
+      launch_gemm_dual(p, s, "bench");
+      ZV_CHECK(hipEventRecord(e0, s));
+      for (int i = 0; i < iters; ++i) launch_gemm_dual(p, s, "bench");
+      ZV_CHECK(hipEventRecord(e1, s));
+      ZV_CHECK(hipEventSynchronize(e1));
+      ZV_CHECK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= iters;
+      ZV_CHECK(hipEventDestroy(e0)); ZV_CHECK(hipEventDestroy(e1));
+      break;
+    }
     default: throw std::invalid_argument("unknown variant");
   }
   *ms_out = ms;
@@ -1446,6 +1472,15 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
   p.Ah = A; p.lda = Kp; p.Bh = W; p.ldb = Kp; p.ldc = N; p.rows_per_group = 1; p.rpb = 1;
   if (mode == 1) p.act = 1;
   float* outs[2] = {C0, C1};
+  float* extra = nullptr;          // dual-group variants: bias, bypass original / scale
+  if (variant == 60 || variant == 61) {
+    if (mode != 2) throw std::invalid_argument("selftest: the dual-group kernel is residual-only");
+    ZV_CHECK(hipMalloc(&extra, (size_t)(2 * N + (size_t)M * N) * 4));
+    hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(4096), dim3(256), 0, s, reinterpret_cast<bf16*>(extra),
+                       (long)(2 * N + (long)M * N) * 2, 4u);
+    p.bias = extra;
+    if (variant == 61) { p.byp = extra + N; p.orig = extra + 2 * N; }
+  }
   // the deferred-store variant writes bf16 only: both runs then write bf16 (into
   // the two halves of R) and are widened into C0 / C1 for the comparison
   const bool bf16_out = variant == 40;
@@ -1470,6 +1505,7 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
       case 22: launch_gemm8<0, EPI_STD, false>(p, s, "t"); break;
       case 23: launch_gemm8<1, EPI_STD, false>(p, s, "t"); break;
       case 50: launch_gemm_pp<128, 128, 2, 4, EPI_STD, 0>(p, s, "t"); break;
+      case 60: case 61: launch_gemm_dual(p, s, "t"); break;
       default: throw std::invalid_argument("selftest: unknown variant");
     }
   }
@@ -1483,6 +1519,7 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
   ZV_CHECK(hipMemcpy(h, res, 8, hipMemcpyDeviceToHost));
   *maxdiff = h[0]; *maxref = h[1];
   for (void* q : {(void*)A, (void*)W, (void*)C0, (void*)C1, (void*)R, (void*)res}) ZV_CHECK(hipFree(q));
+  if (extra) ZV_CHECK(hipFree(extra));
   ZV_API_END
 }
 
