@@ -20,7 +20,6 @@
 #include "zv_gemm.inc"
 #include "zv_gemm_ws.inc"
 #include "zv_gemm_dual.inc"
-#include "zv_gemm8.inc"
 #include "zv_gemm_pp.inc"
 #include "zv_attn.inc"
 #include "zv_elem.inc"
@@ -184,8 +183,6 @@ struct zv_engine {
                                    // term on the MFMA chain (zv_attn_sa_tp_kernel), the head-0
                                    // stats / NonlinAttention scoring too; 0 = VALU forms
                                    // (3: A/B arm, SA with the one-wave register budget)
-  bool sa_pos_mfma = false;        // A/B: ZV_SA_POS_MFMA=1 puts the SelfAttention positional term on
-                                   // f32 MFMA (parity-green, same time: the loop is latency bound)
   bool skinny_tiles = true;        // V^T projection (N = 48) on 64x64 tiles, one per block
                                    // (ZV_GEMM_SKINNY=0: 128x64 persistent arm; a 128x96 tile for
                                    // the N = 272 projection measured slower: profiles/r01_skinny_ab.txt)
@@ -196,21 +193,12 @@ struct zv_engine {
                                    // bf16 hi/lo pair (8 B per update instead of 10): residual GEMMs
                                    // -4..9 %, but the forward is unchanged (other kernels slower,
                                    // profiles/r01_pair_resid_ab.txt); the fp32 stream stays default
-  int fused_tile = 0;              // A/B: ZV_GEMM_FUSED_TILE 1 = GLU / NA in-projections on
-                                   // 256-row 3-stage tiles (one 8-wave block per CU)
-  int gemm_tile = 0;               // ZV_GEMM_TILE 0 (default): 128x128 two blocks per CU; A/B arms
-                                   // (bf16 linears with N >= 256): 1 = 256x128, 2 = 256x256,
-                                   // 3 = 256x128 3-stage, 5 = 256x128 3-stage for the
-                                   // non-residual ones only (same-box in-model A/B within noise:
-                                   // profiles/r01_gemm_tile_ab.txt)
 
   explicit zv_engine(const zv_config& c) : cfg(c) {
     const char* e = getenv("ZV_ATTN_MATERIALIZE");
     materialize_attn = e && e[0] == '1';
     const char* gr = getenv("ZV_GRAPH");
     graphs_enabled = !(gr && gr[0] == '0');
-    const char* g = getenv("ZV_GEMM_TILE");
-    gemm_tile = g ? atoi(g) : 0;
     const char* o1 = getenv("ZV_GEMM_OCC_PLAIN");
     const char* o2 = getenv("ZV_GEMM_OCC_RESID");
     const char* o3 = getenv("ZV_GEMM_OCC_FUSED");
@@ -221,8 +209,6 @@ struct zv_engine {
     gridx_plain = envi("ZV_GEMM_GRIDX_PLAIN", -1);
     gridx_resid = envi("ZV_GEMM_GRIDX_RESID", -1);
     gridx_fused = envi("ZV_GEMM_GRIDX_FUSED", -1);
-    fused_tile = envi("ZV_GEMM_FUSED_TILE", 0);
-    sa_pos_mfma = envi("ZV_SA_POS_MFMA", 0) != 0;
     sa_tp = envi("ZV_SA_TP", 1);
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
@@ -582,26 +568,6 @@ struct zv_engine {
       }
     }
     if constexpr (SPLIT == 1) {
-      if (gemm_tile == 1 && Lw.N >= 256) {
-        launch_gemm<256, 128, 4, 2, SPLIT, EPI_STD>(p, 1, s, tag);
-        return;
-      }
-      if (gemm_tile == 2 && Lw.N >= 256) {
-        launch_gemm<256, 256, 2, 4, SPLIT, EPI_STD>(p, 1, s, tag);
-        return;
-      }
-      if (gemm_tile == 3 && Lw.N >= 256) {
-        launch_gemm<256, 128, 4, 2, SPLIT, EPI_STD, 3>(p, 1, s, tag);
-        return;
-      }
-    }
-    if constexpr (SPLIT == 1) {
-      if (gemm_tile == 5 && !o.resid && Lw.N >= 256) {
-        launch_gemm<256, 128, 4, 2, SPLIT, EPI_STD, 3>(p, 1, s, tag);
-        return;
-      }
-    }
-    if constexpr (SPLIT == 1) {
       // bf16-only outputs on whole tiles: the next tile's K loop does not wait for
       // this tile's stores (counted vmcnt, zv_gemm.inc DEFER)
       if (defer_stores && !o.resid && !o.C && o.act.h && !o.act.l && Lw.N % 128 == 0 &&
@@ -708,8 +674,6 @@ struct zv_engine {
       bool done = false;
       if constexpr (SPLIT == 1)
         if (gemm_pp && W.na_in.N % 192 == 0) { launch_gemm_pp<128, 192, 2, 4, EPI_NA, 0>(p, s, "gemm_bf16_na"); done = true; }
-      if constexpr (SPLIT == 1)
-        if (!done && fused_tile == 1) { launch_gemm<256, 96, 4, 2, SPLIT, EPI_NA, 2, 2>(p, 1, s, "gemm_bf16_na"); done = true; }
       if (done) {}
       else if (occ_fused == 2) launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       else launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 1>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
@@ -769,7 +733,7 @@ struct zv_engine {
         f.oh = o.h; f.ol = o.l; f.ldo = o.ld; f.ocol_per_head = vd;
         bool done = false;
         if constexpr (SPLIT == 1)
-          if (sa_tp && !sa_pos_mfma) {   // positional term as a Toeplitz MFMA product
+          if (sa_tp) {                   // positional term as a Toeplitz MFMA product
             if (sa_tp == 3) {          // A/B: the compiler's one-wave register budget
               if (io_split) launch_attn_sa_tp<1, 1>(f, s);
               else launch_attn_sa_tp<0, 1>(f, s);
@@ -777,9 +741,7 @@ struct zv_engine {
             else launch_attn_sa_tp<0>(f, s);
             done = true;
           }
-        if (done) {}
-        else if (sa_pos_mfma) launch_attn_sa_mf<SPLIT>(f, s);
-        else launch_attn_sa<SPLIT>(f, s);
+        if (!done) launch_attn_sa<SPLIT>(f, s);
       }
       Out e = res;
       if (temb) { e.rowvec = temb; e.rowvec_ld = D; e.rows_per_group = L; }
@@ -792,8 +754,6 @@ struct zv_engine {
       bool done = false;
       if constexpr (SPLIT == 1)
         if (gemm_pp && W.conv_in[c].N % 128 == 0) { launch_gemm_pp<128, 128, 2, 4, EPI_GLU, 0>(p, s, "gemm_bf16_glu"); done = true; }
-      if constexpr (SPLIT == 1)
-        if (!done && fused_tile == 1) { launch_gemm<256, 128, 4, 2, SPLIT, EPI_GLU, 3>(p, 1, s, "gemm_bf16_glu"); done = true; }
       if (done) {}
       else if (occ_fused == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       else launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 1>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
@@ -1222,20 +1182,6 @@ static float bench_variant_pp(GemmParams p, int iters, hipStream_t s) {
   return ms / iters;
 }
 
-template <int ORDER, bool PB>
-static float bench_variant8(GemmParams p, int iters, hipStream_t s) {
-  hipEvent_t e0, e1;
-  ZV_CHECK(hipEventCreate(&e0)); ZV_CHECK(hipEventCreate(&e1));
-  launch_gemm8<ORDER, EPI_STD, PB>(p, s, "bench");
-  ZV_CHECK(hipEventRecord(e0, s));
-  for (int i = 0; i < iters; ++i) launch_gemm8<ORDER, EPI_STD, PB>(p, s, "bench");
-  ZV_CHECK(hipEventRecord(e1, s));
-  ZV_CHECK(hipEventSynchronize(e1));
-  float ms = 0.f;
-  ZV_CHECK(hipEventElapsedTime(&ms, e0, e1));
-  ZV_CHECK(hipEventDestroy(e0)); ZV_CHECK(hipEventDestroy(e1));
-  return ms / iters;
-}
 
 extern "C" {
 
@@ -1395,10 +1341,6 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
     case 31: ms = bench_variant<128, 128, 2, 2, 3, 32>(p, iters, persistent, s); break;
     case 32: ms = bench_variant<256, 128, 2, 2, 2, 32>(p, iters, persistent, s); break;
     case 33: ms = bench_variant<256, 128, 2, 2, 3, 32>(p, iters, persistent, s); break;
-    case 20: ms = bench_variant8<0, true>(p, iters, s); break;
-    case 21: ms = bench_variant8<1, true>(p, iters, s); break;
-    case 22: ms = bench_variant8<0, false>(p, iters, s); break;
-    case 23: ms = bench_variant8<1, false>(p, iters, s); break;
     case 50: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD>(p, iters, s); break;
     case 52: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD, 3>(p, iters, s); break;   // out mode 4 only
     case 53: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD, 4>(p, iters, s); break;   // out mode 4 only
@@ -1500,10 +1442,6 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
     else switch (variant) {
       case 30: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 4, 2, 32>(p, 1, s, "t", true, 0); break;
       case 40: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2, GEMM_BK, 8>(p, 1, s, "t", true, 0); break;
-      case 20: launch_gemm8<0, EPI_STD, true>(p, s, "t"); break;
-      case 21: launch_gemm8<1, EPI_STD, true>(p, s, "t"); break;
-      case 22: launch_gemm8<0, EPI_STD, false>(p, s, "t"); break;
-      case 23: launch_gemm8<1, EPI_STD, false>(p, s, "t"); break;
       case 50: launch_gemm_pp<128, 128, 2, 4, EPI_STD, 0>(p, s, "t"); break;
       case 60: case 61: launch_gemm_dual(p, s, "t"); break;
       default: throw std::invalid_argument("selftest: unknown variant");
