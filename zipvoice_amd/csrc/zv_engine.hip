@@ -599,6 +599,12 @@ struct zv_engine {
       else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 1>(p, 1, s, rtag, true, gridx_resid);
       return;
     }
+    // 96-wide tiles where they waste fewer columns than 128-wide ones (the attention-score
+    // projection, N = 272: 288 computed columns instead of 384)
+    if ((Lw.N + 95) / 96 * 96 < (Lw.N + 127) / 128 * 128) {
+      launch_gemm<128, 96, 2, 2, SPLIT, EPI_STD, 2, 2>(p, 1, s, SPLIT == 3 ? "gemm_fp32_n96" : "gemm_bf16_n96", true, gridx_plain);
+      return;
+    }
     if (occ_plain == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2>(p, 1, s, tag, true, gridx_plain);
     else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1>(p, 1, s, tag, true, gridx_plain);
   }
