@@ -62,8 +62,10 @@ def up_to_date(out=OUT, defines=()):
 
 def _cmd(out, defines):
     digest = source_hash(defines)
+    # ZV_EXTRA_FLAGS: extra compiler flags for alternative builds (A/B runs with --out)
+    extra = os.environ.get("ZV_EXTRA_FLAGS", "").split()
     return digest, [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                    "-munsafe-fp-atomics", "-Wno-unused-result", "-Wl,-Bsymbolic",
+                    "-munsafe-fp-atomics", "-Wno-unused-result", "-Wl,-Bsymbolic", *extra,
                     *[f"-D{d}" for d in defines], f'-DZV_SRC_HASH="{digest}"', "-o", out + ".tmp",
                     SRC]
 
