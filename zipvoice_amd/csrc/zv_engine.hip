@@ -189,6 +189,8 @@ struct zv_engine {
   bool defer_stores = false;       // A/B: ZV_GEMM_DEFER=1 lets the next tile's K loop run past the
                                    // plain bf16 linears' stores (bitwise equal; up to 6 % in isolation,
                                    // ~1 % slower in the model: profiles/r01_gemm_defer_ab.txt)
+  bool res_counted = true;         // A/B: ZV_RES_COUNTED=0 runs the residual linears through the
+                                   // general epilogue (zv_gemm.inc gemm_epilogue)
   bool pair_resid = false;         // A/B: ZV_PAIR_RESID=1 carries the bf16-mode residual stream as a
                                    // bf16 hi/lo pair (8 B per update instead of 10): residual GEMMs
                                    // -4..9 %, but the forward is unchanged (other kernels slower,
@@ -213,6 +215,7 @@ struct zv_engine {
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
+    res_counted = envi("ZV_RES_COUNTED", 1) != 0;
     resid_ws = envi("ZV_RESID_WS", 1);
     gemm_pp = envi("ZV_GEMM_PP", 0);
     gemm_dual = envi("ZV_GEMM_DUAL", 0);
@@ -595,8 +598,21 @@ struct zv_engine {
           launch_gemm_resid_ws(p, s, "gemm_bf16_resid_ws");   // own tag: one symbol per roofline tag
           return;
         }
-      if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 1>(p, 1, s, rtag, true, gridx_resid);
-      else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 1>(p, 1, s, rtag, true, gridx_resid);
+      // the counted residual epilogue (zv_gemm.inc gemm_epilogue_res; ROLE 2 = with the
+      // bypass original) where its preconditions hold, else the general epilogue
+      const bool counted = res_counted && p.bias && !p.rowvec && !p.act && Lw.N % 8 == 0 &&
+                           p.ldc % 4 == 0 && (!p.Ch || p.ldch % 8 == 0) && (!p.orig || p.byp) &&
+                           (p.Cl != nullptr) == (SPLIT == 3 && p.Ch != nullptr);
+      if (!counted) {
+        if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2>(p, 1, s, rtag, true, gridx_resid);
+        else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1>(p, 1, s, rtag, true, gridx_resid);
+      } else if (p.orig) {
+        if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 2>(p, 1, s, rtag, true, gridx_resid);
+        else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 2>(p, 1, s, rtag, true, gridx_resid);
+      } else {
+        if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 1>(p, 1, s, rtag, true, gridx_resid);
+        else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 1>(p, 1, s, rtag, true, gridx_resid);
+      }
       return;
     }
     // 96-wide tiles where they waste fewer columns than 128-wide ones (the attention-score
@@ -1157,14 +1173,14 @@ static __global__ void zv_fill_rand_bf16(bf16* p, long n, unsigned seed) {
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int STAGES, int BK = GEMM_BK, int DEFER = 0>
+template <int BM, int BN, int WGM, int WGN, int STAGES, int BK = GEMM_BK, int DEFER = 0, int ROLE = 0>
 static float bench_variant(GemmParams p, int iters, bool persistent, hipStream_t s) {
   hipEvent_t e0, e1;
   ZV_CHECK(hipEventCreate(&e0)); ZV_CHECK(hipEventCreate(&e1));
-  launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES, 2, BK, DEFER>(p, 1, s, "bench", persistent);
+  launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES, 2, BK, DEFER, 0, 0, ROLE>(p, 1, s, "bench", persistent);
   ZV_CHECK(hipEventRecord(e0, s));
   for (int i = 0; i < iters; ++i)
-    launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES, 2, BK, DEFER>(p, 1, s, "bench", persistent);
+    launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES, 2, BK, DEFER, 0, 0, ROLE>(p, 1, s, "bench", persistent);
   ZV_CHECK(hipEventRecord(e1, s));
   ZV_CHECK(hipEventSynchronize(e1));
   float ms = 0.f;
@@ -1329,6 +1345,15 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
   if (out_mode == 2) p.resid = C;
   if (out_mode == 3) p.act = 1;
   if (out_mode == 4) { p.C = nullptr; p.Ch = nullptr; }
+  float* extra = nullptr;          // modes 5 / 6: a residual linear's epilogue operands
+  if (out_mode == 5 || out_mode == 6) {
+    ZV_CHECK(hipMalloc(&C, (size_t)M * N * 4));
+    ZV_CHECK(hipMemsetAsync(C, 0, (size_t)M * N * 4, s));
+    ZV_CHECK(hipMalloc(&extra, (size_t)(2 * N + (out_mode == 6 ? (size_t)M * N : 0)) * 4));
+    ZV_CHECK(hipMemsetAsync(extra, 0, (size_t)(2 * N + (out_mode == 6 ? (size_t)M * N : 0)) * 4, s));
+    p.C = C; p.resid = C; p.bias = extra;
+    if (out_mode == 6) { p.byp = extra + N; p.orig = extra + 2 * N; }
+  }
   float ms = -1.f;
   switch (variant) {
     case 0: ms = bench_variant<128, 128, 2, 2, 2>(p, iters, persistent, s); break;
@@ -1350,6 +1375,12 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
     case 50: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD>(p, iters, s); break;
     case 52: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD, 3>(p, iters, s); break;   // out mode 4 only
     case 53: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD, 4>(p, iters, s); break;   // out mode 4 only
+    case 70: {                     // counted residual epilogue (out modes 5 / 6)
+      if (out_mode != 5 && out_mode != 6) throw std::invalid_argument("variant 70: modes 5 / 6 only");
+      ms = out_mode == 5 ? bench_variant<128, 128, 2, 2, 2, GEMM_BK, 0, 1>(p, iters, persistent, s)
+                         : bench_variant<128, 128, 2, 2, 2, GEMM_BK, 0, 2>(p, iters, persistent, s);
+      break;
+    }
     case 60: {                     // dual-group residual kernel (out mode 2 only)
       if (out_mode != 2) throw std::invalid_argument("variant 60: residual mode only");
       hipEvent_t e0, e1;
@@ -1368,6 +1399,7 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
   }
   *ms_out = ms;
   ZV_CHECK(hipFree(A)); ZV_CHECK(hipFree(W));
+  if (extra) ZV_CHECK(hipFree(extra));
   if (C) ZV_CHECK(hipFree(C));
   if (Ch) ZV_CHECK(hipFree(Ch));
   ZV_API_END
@@ -1421,13 +1453,13 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
   if (mode == 1) p.act = 1;
   float* outs[2] = {C0, C1};
   float* extra = nullptr;          // dual-group variants: bias, bypass original / scale
-  if (variant == 60 || variant == 61) {
-    if (mode != 2) throw std::invalid_argument("selftest: the dual-group kernel is residual-only");
+  if (variant == 60 || variant == 61 || variant == 70 || variant == 71) {
+    if (mode != 2) throw std::invalid_argument("selftest: residual-only variant");
     ZV_CHECK(hipMalloc(&extra, (size_t)(2 * N + (size_t)M * N) * 4));
     hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(4096), dim3(256), 0, s, reinterpret_cast<bf16*>(extra),
                        (long)(2 * N + (long)M * N) * 2, 4u);
     p.bias = extra;
-    if (variant == 61) { p.byp = extra + N; p.orig = extra + 2 * N; }
+    if (variant == 61 || variant == 71) { p.byp = extra + N; p.orig = extra + 2 * N; }
   }
   // the deferred-store variant writes bf16 only: both runs then write bf16 (into
   // the two halves of R) and are widened into C0 / C1 for the comparison
@@ -1450,6 +1482,9 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
       case 40: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2, GEMM_BK, 8>(p, 1, s, "t", true, 0); break;
       case 50: launch_gemm_pp<128, 128, 2, 4, EPI_STD, 0>(p, s, "t"); break;
       case 60: case 61: launch_gemm_dual(p, s, "t"); break;
+      // the counted residual epilogue (ROLE 1 / 2) against the general one
+      case 70: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 1>(p, 1, s, "t", true, -1); break;
+      case 71: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 2>(p, 1, s, "t", true, -1); break;
       default: throw std::invalid_argument("selftest: unknown variant");
     }
   }
