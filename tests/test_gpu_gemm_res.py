@@ -1,10 +1,11 @@
-"""The counted residual epilogue (zv_gemm.inc gemm_epilogue_res, the residual-stream
-linears' ROLE 1 / 2 kernels: every epilogue load and store unconditional, stores outside
-the output to a sink) against the general epilogue it replaces: same arithmetic in the
-same order, so bitwise equal -- per launch on random operands (bias + fp32 residual
-read-modify-write, variant 70; + bypass original / scale, variant 71; ragged M and N,
-K = 64 .. 1920) and for the decoder forward in the bf16 and fp32 modes and the Distill
-variant (ZV_RES_COUNTED=1 vs 0)."""
+"""The counted GEMM epilogue (zv_gemm.inc gemm_epilogue_res: the residual-stream linears'
+ROLE 1 / 2 kernels and the plain linears' ROLE 3; every epilogue load and store
+unconditional, stores outside the output to a sink) against the general epilogue it
+replaces: same arithmetic in the same order, so bitwise equal -- per launch on random
+operands (bias + fp32 residual read-modify-write, variant 70; + bypass original / scale,
+variant 71; bias (+ SwooshL) -> bf16, variant 72; ragged M and N, K = 64 .. 1920) and for
+the decoder forward in the bf16 and fp32 modes and the Distill variant
+(ZV_RES_COUNTED=1 vs 0)."""
 import ctypes
 
 import numpy as np
@@ -29,6 +30,18 @@ def test_counted_epilogue_launch_bitwise(M, N, K, variant):
     assert rc == 0, lib.zv_last_error().decode()
     print(f"M={M} N={N} K={K} v={variant}: maxdiff {d.value:.3e} (|ref| {r.value:.3e})")
     assert d.value == 0.0, (M, N, K, variant, d.value)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("M,N,K", SHAPES[:4] + [(78016, 1536, 512), (3001, 272, 512)])
+def test_counted_plain_epilogue_launch_bitwise(M, N, K, mode):
+    from zipvoice_amd import engine
+    lib = engine.load_library()
+    d, r = ctypes.c_float(), ctypes.c_float()
+    rc = lib.zv_gemm_selftest(M, N, K, 72, mode, ctypes.byref(d), ctypes.byref(r))
+    assert rc == 0, lib.zv_last_error().decode()
+    print(f"M={M} N={N} K={K} v=72 mode={mode}: maxdiff {d.value:.3e} (|ref| {r.value:.3e})")
+    assert d.value == 0.0, (M, N, K, mode, d.value)
 
 
 @pytest.mark.parametrize("variant,precision", [("zipvoice", "bf16"), ("zipvoice", "fp32"),

@@ -621,8 +621,17 @@ struct zv_engine {
       launch_gemm<128, 96, 2, 2, SPLIT, EPI_STD, 2, 2>(p, 1, s, SPLIT == 3 ? "gemm_fp32_n96" : "gemm_bf16_n96", true, gridx_plain);
       return;
     }
-    if (occ_plain == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2>(p, 1, s, tag, true, gridx_plain);
-    else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1>(p, 1, s, tag, true, gridx_plain);
+    // bias (+ activation) -> bf16 copy: the counted epilogue (ROLE 3)
+    const bool counted = res_counted && p.bias && p.Ch && !p.C && !p.rowvec && Lw.N % 8 == 0 &&
+                         p.ldch % 8 == 0 && (p.Cl != nullptr) == (SPLIT == 3);
+    if (counted) {
+      if (occ_plain == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, tag, true, gridx_plain);
+      else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 3>(p, 1, s, tag, true, gridx_plain);
+    } else if (occ_plain == 2) {
+      launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2>(p, 1, s, tag, true, gridx_plain);
+    } else {
+      launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1>(p, 1, s, tag, true, gridx_plain);
+    }
   }
 
   // ---------------------------------------------------------------- one layer
@@ -697,6 +706,8 @@ struct zv_engine {
       if constexpr (SPLIT == 1)
         if (gemm_pp && W.na_in.N % 192 == 0) { launch_gemm_pp<128, 192, 2, 4, EPI_NA, 0>(p, s, "gemm_bf16_na"); done = true; }
       if (done) {}
+      else if (res_counted && occ_fused == 2 && p.bias && W.na_in.N % 48 == 0 && p.ldch % 4 == 0)
+        launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       else if (occ_fused == 2) launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       else launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 1>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       Act nao = ws.na_o.get(M, round_up(hid, 64), split);
@@ -738,7 +749,9 @@ struct zv_engine {
       GemmParams p = gp_linear(W.sa_in[a], cur_a, M);
       p.Cth = vt.h; p.Ctl = vt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)HV * Lpad;
       // N = 48: 64-row tiles give 2x the blocks of a 128-row grid (one tile column)
-      if (skinny_tiles) launch_gemm<64, 64, 2, 2, SPLIT, EPI_TRANS>(p, 1, s, split ? "gemm_fp32_t" : "gemm_bf16_t", true, -1);
+      if (skinny_tiles && res_counted)
+        launch_gemm<64, 64, 2, 2, SPLIT, EPI_TRANS, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, split ? "gemm_fp32_t" : "gemm_bf16_t", true, -1);
+      else if (skinny_tiles) launch_gemm<64, 64, 2, 2, SPLIT, EPI_TRANS>(p, 1, s, split ? "gemm_fp32_t" : "gemm_bf16_t", true, -1);
       else launch_gemm<128, 64, 2, 2, SPLIT, EPI_TRANS>(p, 1, s, split ? "gemm_fp32_t" : "gemm_bf16_t");
       if (materialize) {
         GemmParams q{};
@@ -777,6 +790,8 @@ struct zv_engine {
       if constexpr (SPLIT == 1)
         if (gemm_pp && W.conv_in[c].N % 128 == 0) { launch_gemm_pp<128, 128, 2, 4, EPI_GLU, 0>(p, s, "gemm_bf16_glu"); done = true; }
       if (done) {}
+      else if (res_counted && occ_fused == 2 && p.bias && W.conv_in[c].N % 32 == 0 && p.ldch % 8 == 0)
+        launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       else if (occ_fused == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       else launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 1>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       Act dw = ws.dw.get(M, D, split);
@@ -1346,6 +1361,11 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
   if (out_mode == 3) p.act = 1;
   if (out_mode == 4) { p.C = nullptr; p.Ch = nullptr; }
   float* extra = nullptr;          // modes 5 / 6: a residual linear's epilogue operands
+  if (out_mode == 7) {             // a plain linear's: bias + SwooshL -> bf16 copy
+    ZV_CHECK(hipMalloc(&extra, (size_t)N * 4));
+    ZV_CHECK(hipMemsetAsync(extra, 0, (size_t)N * 4, s));
+    p.C = nullptr; p.bias = extra; p.act = 1;
+  }
   if (out_mode == 5 || out_mode == 6) {
     ZV_CHECK(hipMalloc(&C, (size_t)M * N * 4));
     ZV_CHECK(hipMemsetAsync(C, 0, (size_t)M * N * 4, s));
@@ -1375,6 +1395,11 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
     case 50: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD>(p, iters, s); break;
     case 52: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD, 3>(p, iters, s); break;   // out mode 4 only
     case 53: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD, 4>(p, iters, s); break;   // out mode 4 only
+    case 72: {                     // counted plain epilogue (out mode 7)
+      if (out_mode != 7) throw std::invalid_argument("variant 72: mode 7 only");
+      ms = bench_variant<128, 128, 2, 2, 2, GEMM_BK, 0, 3>(p, iters, persistent, s);
+      break;
+    }
     case 70: {                     // counted residual epilogue (out modes 5 / 6)
       if (out_mode != 5 && out_mode != 6) throw std::invalid_argument("variant 70: modes 5 / 6 only");
       ms = out_mode == 5 ? bench_variant<128, 128, 2, 2, 2, GEMM_BK, 0, 1>(p, iters, persistent, s)
@@ -1453,6 +1478,12 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
   if (mode == 1) p.act = 1;
   float* outs[2] = {C0, C1};
   float* extra = nullptr;          // dual-group variants: bias, bypass original / scale
+  if (variant == 72) {             // counted plain epilogue: bias (+ SwooshL) -> bf16
+    ZV_CHECK(hipMalloc(&extra, (size_t)N * 4));
+    hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(64), dim3(256), 0, s, reinterpret_cast<bf16*>(extra),
+                       (long)N * 2, 5u);
+    p.bias = extra;
+  }
   if (variant == 60 || variant == 61 || variant == 70 || variant == 71) {
     if (mode != 2) throw std::invalid_argument("selftest: residual-only variant");
     ZV_CHECK(hipMalloc(&extra, (size_t)(2 * N + (size_t)M * N) * 4));
@@ -1463,7 +1494,7 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
   }
   // the deferred-store variant writes bf16 only: both runs then write bf16 (into
   // the two halves of R) and are widened into C0 / C1 for the comparison
-  const bool bf16_out = variant == 40;
+  const bool bf16_out = variant == 40 || variant == 72;
   if (bf16_out && mode == 2) throw std::invalid_argument("selftest: variant 40 has no residual form");
   for (int k = 0; k < 2; ++k) {
     p.C = outs[k];
@@ -1485,6 +1516,7 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
       // the counted residual epilogue (ROLE 1 / 2) against the general one
       case 70: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 1>(p, 1, s, "t", true, -1); break;
       case 71: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 2>(p, 1, s, "t", true, -1); break;
+      case 72: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, "t", true, -1); break;
       default: throw std::invalid_argument("selftest: unknown variant");
     }
   }
