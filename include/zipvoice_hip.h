@@ -58,8 +58,12 @@ enum zv_variant { ZV_ZIPVOICE = 0, ZV_DISTILL = 1, ZV_DIALOG = 2, ZV_DIALOG_STER
  *          output).
  * The 16-bit operand format is the library's: bf16 in libzipvoice_hip.so, IEEE fp16 in
  * libzipvoice_hip_f16.so (same entry points, built from the same sources with
- * -DZV_OPERAND_F16).  ZV_MIXED in the fp16 library is the parity-grade fast mode. */
-enum zv_precision { ZV_FP32 = 0, ZV_BF16 = 1, ZV_MIXED = 2 };
+ * -DZV_OPERAND_F16).  ZV_MIXED in the fp16 library is the parity-grade fast mode.
+ * ZV_FP8: ZV_BF16 with the decoder layers' feed-forward, convolution-module and
+ *          NonlinAttention output linears on block-scaled MX-fp8 MFMA (e4m3 weights and
+ *          activations, one power-of-two scale per 32 K elements; bf16 library only).  The
+ *          BASELINE C5 "fp8 MFMA weights" mode, with its own tolerance. */
+enum zv_precision { ZV_FP32 = 0, ZV_BF16 = 1, ZV_MIXED = 2, ZV_FP8 = 3 };
 
 #define ZV_MAX_STACKS 8
 
@@ -118,6 +122,19 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
  * 256x256 phased kernel) against the 128x128 kernel on the same random operands,
  * fp32 C; mode 0 plain, 1 SwooshL, 2 residual.  Writes max |diff| and max |ref|. */
 int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff, float* maxref);
+
+/* MX-fp8 operand format of the fp8 mode (csrc/zv_mx8.inc): e4m3 values, one E8M0 scale byte per
+ * 32 consecutive K elements.  zv_mx8_quantize: the host quantiser the engine applies to the
+ * fp8 weights (host pointers, no GPU: x (rows, K) fp32 -> q (rows, ldq), s (rows, ldq / 32),
+ * ldq = K rounded up to 128).  zv_mx8_gemm_check: the fp8 GEMM end to end on the device (host
+ * pointers in and out): A (M, K) is rounded to bf16 and quantised by the device producer kernel
+ * (zv_mx8_pack_kernel; its output returned in Aq / As), W (N, K) by the host quantiser, and
+ * C = A8 . W8^T through the block-scaled MFMA GEMM with the residual epilogue (zero residual
+ * and bias), K a multiple of 128.  Both replace no reference interface: they pin the fp8
+ * mode's operand format and GEMM against tests/ (numpy). */
+int zv_mx8_quantize(const float* x, int rows, int K, uint8_t* q, uint8_t* s);
+int zv_mx8_gemm_check(int M, int N, int K, const float* A, const float* W, float* C, uint8_t* Aq,
+                      uint8_t* As);
 
 /* Raw decoder: v = fm_decoder(cat[xt, text_c, speech_c], t, pad, g).
  *  t:      [N] timesteps;  guidance: [N] (distill only, else NULL)

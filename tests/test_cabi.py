@@ -12,7 +12,7 @@ HEADER = os.path.join(REPO, "include", "zipvoice_hip.h")
 def declared_symbols():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(zv_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(zv_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_header_declares_api():
@@ -96,3 +96,35 @@ def test_gpu_box_library_provenance():
     from zipvoice_amd.csrc.build import VARIANTS, library_hash, source_hash
     for out, defines in VARIANTS:
         assert library_hash(out) == source_hash(defines), f"stale {out}"
+
+
+def test_mx8_host_quantizer_matches_numpy_spec():
+    """The fp8 mode's weight quantiser (csrc/zv_mx8.inc mx8_quantize_host, through the C ABI;
+    host only, no GPU) is bit-exact to the numpy specification oracle/mx8_np.py: e4m3 codes
+    and E8M0 scale bytes, including zero blocks, subnormal-range values, the 448 maximum,
+    rounding ties and a ragged K padded to 128."""
+    import numpy as np
+    from oracle import mx8_np
+    from zipvoice_amd import engine
+    lib = engine.load_library()
+    rng = np.random.default_rng(7)
+    rows, K = 9, 200
+    x = rng.standard_normal((rows, K)).astype(np.float32)
+    x *= np.exp2(rng.integers(-30, 30, (rows, 1))).astype(np.float32)
+    x[0, :32] = 0.0                                   # a zero block
+    x[1, :] *= 1e-38                                  # subnormal-range inputs
+    x[2, :32] = 448.0 * np.linspace(-1, 1, 32)        # exactly at the e4m3 maximum
+    x[3, :16] = np.float32(1.0625)                    # a tie between two e4m3 codes (1.0 / 1.125)
+    x[3, 16:32] = np.float32(448.0)
+    ldq = 256
+    q = np.zeros((rows, ldq), np.uint8)
+    s = np.zeros((rows, ldq // 32), np.uint8)
+    assert lib.zv_mx8_quantize(x.ctypes.data, rows, K, q.ctypes.data, s.ctypes.data) == 0
+    rq, rs = mx8_np.quantize(x, ldq)
+    assert np.array_equal(s, rs)
+    assert np.array_equal(q, rq)
+    # the format round trip: relative error within e4m3's half step of the block maximum
+    y = mx8_np.dequantize(q, s)[:, :K]
+    blk = np.abs(np.pad(x, ((0, 0), (0, ldq - K)))).reshape(rows, -1, 32).max(2)
+    bound = np.repeat(blk, 32, axis=1)[:, :K] * 2.0 ** -4
+    assert (np.abs(y - x) <= bound + 1e-45).all()

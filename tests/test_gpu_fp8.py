@@ -1,0 +1,140 @@
+"""The fp8 mode (precision="fp8", ZV_FP8): BASELINE.json configs[4] "ZipVoice-Dialog-Stereo ...
+fp8 MFMA weights".  The decoder layers' feed-forward (in + out), convolution-module (in + out)
+and NonlinAttention output linears run on gfx950's block-scaled MFMA
+(v_mfma_scale_f32_16x16x128_f8f6f4) with MX-fp8 operands: e4m3 values and one E8M0 scale per
+32 K elements (csrc/zv_mx8.inc), weights quantised once at load, activations by their
+producers (GEMM epilogues or the pack kernel).  Everything else is the bf16 mode.
+
+1. The operand format and the GEMM against the numpy specification (oracle/mx8_np.py):
+   device-quantised activations bit-exact, the GEMM within the MFMA's own rounding
+   (|err| <= GEMM_RTOL * sum |a*b|) of the exact product of the dequantised operands.
+2. The whole mode against the fp32 oracle at the C5 and C2 shapes.  The reference has no fp8
+   path, so the bar is this mode's own documented tolerance: TOL_FP8 below.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+# mean / max |velocity error| vs the fp32 oracle (the bf16 mode's bar is 5e-2 / 0.25).  Measured
+# (round 2): C5 T=3376 4.0e-2 / 0.28, C2 2.9e-2 / 0.18, short 2.3e-2 / 0.13 - about 3x the bf16
+# mode's error on the same inputs (1.3e-2, 9.8e-3, 7.9e-3)
+TOL_FP8 = (6e-2, 0.5)
+# the block-scaled MFMA's own rounding: its sum of 128 exact fp8 products per instruction is
+# not exact (measured up to 1.2e-4 of sum |a*b| with block scales spread over 2^14,
+# tools/probe/mx8_probe.hip; 2.3e-5 at K = 128 with a 1e-3 block here)
+GEMM_RTOL = 2e-4
+
+
+def bf16_round(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(torch.bfloat16).float().numpy()
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 264, 512), (1000, 512, 1536), (129, 1152, 128),
+                                   (77, 512, 1920)])
+def test_mx8_gemm_vs_numpy_spec(M, N, K):
+    from oracle import mx8_np
+    from zipvoice_amd import engine
+    lib = engine.load_library()
+    rng = np.random.default_rng(M + N + K)
+    A = (rng.standard_normal((M, K)) * np.exp2(rng.integers(-8, 8, (M, 1)))).astype(np.float32)
+    A[:, :32] *= 1e-3                      # blocks of very different magnitude in one row
+    W = (0.05 * rng.standard_normal((N, K))).astype(np.float32)
+    C = np.zeros((M, N), np.float32)
+    Aq = np.zeros((M, K), np.uint8)
+    As = np.zeros((M, K // 32), np.uint8)
+    rc = lib.zv_mx8_gemm_check(M, N, K, A.ctypes.data, W.ctypes.data, C.ctypes.data, Aq.ctypes.data,
+                               As.ctypes.data)
+    assert rc == 0, lib.zv_last_error().decode()
+    rq, rs = mx8_np.quantize(bf16_round(A))
+    assert np.array_equal(As, rs), "device scale bytes differ from the specification"
+    bad = int((Aq != rq).sum())
+    assert bad == 0, f"{bad} device e4m3 codes differ from the specification"
+    wq, ws = mx8_np.quantize(W)
+    a, w = mx8_np.dequantize(rq, rs), mx8_np.dequantize(wq, ws)
+    ref = a @ w.T
+    mag = np.abs(a) @ np.abs(w).T
+    err = np.abs(C - ref)
+    print(f"MX-fp8 GEMM M={M} N={N} K={K}: max |err| / sum|a*b| = {(err / (mag + 1e-30)).max():.2e}")
+    assert (err <= GEMM_RTOL * mag + 1e-30).all()
+
+
+_models, _refs = {}, {}
+
+
+def model(variant, precision):
+    key = (variant, precision)
+    if key not in _models:
+        from zipvoice_amd.config import default_config
+        from zipvoice_amd.models import build_model
+        from zipvoice_amd.weights import synthetic_state_dict
+        cfg = default_config(variant)
+        m = build_model(cfg, precision=precision)
+        m.load_state_dict(synthetic_state_dict(cfg, 0))
+        _models[key] = m.to("cuda:0")
+    return _models[key]
+
+
+def cuda(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0")
+
+
+CASES = {
+    # name: (variant, B, T, lens, Fx, t, g)
+    "C5": ("zipvoice_dialog_stereo", 1, 3376, [3376], 200, 0.4, 1.5),
+    "C2": ("zipvoice", 2, 1219, [1219, 1004], 100, 0.3, 1.0),
+    "C1s": ("zipvoice", 2, 211, [211, 150], 100, 0.7, 1.0),
+}
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_fp8_velocity_vs_oracle(name):
+    from oracle.zipvoice_np import ZipVoiceOracle
+    from zipvoice_amd.config import default_config
+    from zipvoice_amd.weights import synthetic_state_dict
+    variant, B, T, lens, Fx, t, g = CASES[name]
+    rng = np.random.default_rng(int(name[1]))
+    x = rng.standard_normal((B, T, Fx), dtype=np.float32)
+    tc = rng.standard_normal((B, T, 100), dtype=np.float32)
+    sc = (0.3 * rng.standard_normal((B, T, Fx)) - 0.5).astype(np.float32)
+    pm = np.arange(T)[None] >= np.array(lens)[:, None]
+    outs = {p: model(variant, p).engine.velocity(t, g, cuda(x), cuda(tc), cuda(sc), cuda(pm)).cpu().numpy()
+            for p in ("fp8", "bf16")}
+    cfg = default_config(variant)
+    ref = ZipVoiceOracle(cfg, synthetic_state_dict(cfg, 0)).velocity(np.float32(t), x, tc, sc, pm, g)
+    e8, e16 = np.abs(outs["fp8"] - ref), np.abs(outs["bf16"] - ref)
+    print(f"{name} B={B} T={T}: fp8 mean={e8.mean():.3e} max={e8.max():.3e} | "
+          f"bf16 mean={e16.mean():.3e} max={e16.max():.3e} | ref mean|v|={np.abs(ref).mean():.3f}")
+    assert np.isfinite(outs["fp8"]).all()
+    assert e8.mean() < TOL_FP8[0] and e8.max() < TOL_FP8[1]
+
+
+def test_fp8_rows_independent_and_split_streams_bitwise(monkeypatch):
+    """Batched rows equal single-utterance runs (rows never interact), and the split-stream
+    decoder is bitwise equal to one stream in the fp8 mode too."""
+    rng = np.random.default_rng(5)
+    B, T = 4, 300
+    x = rng.standard_normal((B, T, 100), dtype=np.float32)
+    tc = rng.standard_normal((B, T, 100), dtype=np.float32)
+    sc = rng.standard_normal((B, T, 100), dtype=np.float32)
+    outs = []
+    for streams in ("1", "3"):
+        monkeypatch.setenv("ZV_SPLIT_STREAMS", streams)
+        monkeypatch.setenv("ZV_SPLIT_MIN_ROWS", "1")
+        from zipvoice_amd.config import default_config
+        from zipvoice_amd.models import build_model
+        from zipvoice_amd.weights import synthetic_state_dict
+        cfg = default_config("zipvoice")
+        m = build_model(cfg, precision="fp8")
+        m.load_state_dict(synthetic_state_dict(cfg, 0))
+        m = m.to("cuda:0")
+        outs.append(m.engine.velocity(0.3, 1.0, cuda(x), cuda(tc), cuda(sc), None).cpu())
+        if streams == "1":
+            v1 = m.engine.velocity(0.3, 1.0, cuda(x[2:3]), cuda(tc[2:3]), cuda(sc[2:3]), None).cpu()
+            d = (outs[0][2:3] - v1).abs().max().item()
+            print(f"fp8 row 2 batched vs single: {d:.3e}")
+            assert d < 1e-5
+        del m
+    assert torch.equal(outs[0], outs[1])

@@ -8,9 +8,11 @@ conditions, the guided / distilled Euler loop; no vocoder):
   C4  ZipVoice-Dialog, N_steps=16, 16 x (6 s prompt + 30 s generated, T = 3376),
       CFG 1.5 (32 rows)
   C5  ZipVoice-Dialog-Stereo, N_steps=16, 4 per GPU (32 over 8 GPUs), T = 3376,
-      200-dim two-channel features, CFG 1.5 (bf16 weights: fp8 is not built)
+      200-dim two-channel features, CFG 1.5; run it with precision fp8 for the BASELINE
+      "fp8 MFMA weights" mode (ZV_FP8: MX-fp8 feed-forward / conv / NA-out linears)
 
-usage: config_bench.py [C3,C4,C5] [steps]"""
+usage: config_bench.py [C3,C4,C5] [steps] [precision (bf16)]
+Two untimed warm-up steps (the first sizes the workspace, the second captures the graph)."""
 import json
 import os
 import sys
@@ -32,11 +34,11 @@ CONFIGS = {
 }
 
 
-def run(name, steps):
+def run(name, steps, precision="bf16"):
     c = CONFIGS[name]
     dev = torch.device("cuda:0")
     cfg = default_config(c["variant"])
-    m = build_model(cfg, precision="bf16")
+    m = build_model(cfg, precision=precision)
     m.load_state_dict(synthetic_state_dict(cfg, 0))
     m = m.to(dev)
     rng = np.random.default_rng(7)
@@ -61,6 +63,7 @@ def run(name, steps):
                         duration="real", num_step=c["N"], guidance_scale=c["g"])
 
     step()
+    step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -69,7 +72,7 @@ def run(name, steps):
     dt = (time.perf_counter() - t0) / steps
     frames = B * c["Tg"]
     audio_s = frames * 256 / 24000
-    return {"config": name, "variant": c["variant"], "utterances_per_gpu": B, "T": c["Tp"] + c["Tg"],
+    return {"config": name, "variant": c["variant"], "precision": precision, "utterances_per_gpu": B, "T": c["Tp"] + c["Tg"],
             "num_step": c["N"], "ms_per_step": round(dt * 1e3, 2),
             "mel_frames_per_s_per_gpu": round(frames / dt, 1), "x_realtime_per_gpu": round(audio_s / dt, 1)}
 
@@ -77,5 +80,6 @@ def run(name, steps):
 if __name__ == "__main__":
     names = sys.argv[1].split(",") if len(sys.argv) > 1 else list(CONFIGS)
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+    prec = sys.argv[3] if len(sys.argv) > 3 else "bf16"
     for n in names:
-        print(json.dumps(run(n, steps)), flush=True)
+        print(json.dumps(run(n, steps, prec)), flush=True)

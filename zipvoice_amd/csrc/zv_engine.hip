@@ -38,6 +38,9 @@ struct Linear {
   int N = 0, K = 0, Npad = 0, Kpad = 0;
   bf16* hi = nullptr;
   bf16* lo = nullptr;
+  uint8_t* q8 = nullptr;  // fp8 mode: MX-fp8 weight [Npad][Kq] + scales [Npad][Kq / 32] (zv_mx8.inc)
+  uint8_t* s8 = nullptr;
+  int Kq = 0;
   float* w32 = nullptr;   // fp32 copy (small linears only)
   float* b = nullptr;
 };
@@ -104,18 +107,28 @@ struct Act {           // GEMM operand in HBM: bf16 hi (+ lo in fp32-accurate mo
   bf16* h = nullptr;
   bf16* l = nullptr;
   long ld = 0;
+  // fp8 mode: the MX-fp8 copy (values (rows, ldq), scales (rows, ldq / 32)) or null
+  uint8_t* q = nullptr;
+  uint8_t* qs = nullptr;
+  long ldq = 0;
 };
 
 struct ActBuf {
-  DBuf h, l;
-  Act get(long rows, long ld, bool split) {
+  DBuf h, l, q, qs;
+  // fp8: also the MX-fp8 copy of the first `cols` columns; with16 = false: that copy only
+  Act get(long rows, long ld, bool split, bool fp8 = false, long cols = 0, bool with16 = true) {
     Act a;
     a.ld = ld;
-    a.h = h.get<bf16>((size_t)rows * ld);
+    a.h = with16 ? h.get<bf16>((size_t)rows * ld) : nullptr;
     a.l = split ? l.get<bf16>((size_t)rows * ld) : nullptr;
+    if (fp8) {
+      a.ldq = round_up(cols ? cols : ld, MX8_KSTEP);
+      a.q = q.get<uint8_t>((size_t)rows * a.ldq);
+      a.qs = qs.get<uint8_t>((size_t)rows * a.ldq / MX8_BLOCK);
+    }
     return a;
   }
-  size_t bytes() const { return h.bytes + l.bytes; }
+  size_t bytes() const { return h.bytes + l.bytes + q.bytes + qs.bytes; }
 };
 
 struct Workspace {
@@ -123,13 +136,14 @@ struct Workspace {
   DBuf main, dsrc, cur, temb0, temb1, tstack, tvec, gvec, posP, mask2, maskds, vout, stats;
   // bf16 (hi/lo) GEMM operands
   ActBuf xin, main_a, dsrc_a, cur_a, qkp, W, hidden, na_y, na_xt, na_o, sa_vt, sa_o, glu, dw, emb;
+  ActBuf cur8;   // fp8 mode: the working stream's MX-fp8 copy
   size_t bytes() const {
     size_t s = 0;
     for (const DBuf* b : {&main, &dsrc, &cur, &temb0, &temb1, &tstack, &tvec, &gvec, &posP, &mask2,
                           &maskds, &vout, &stats})
       s += b->bytes;
     for (const ActBuf* b : {&xin, &main_a, &dsrc_a, &cur_a, &qkp, &W, &hidden, &na_y, &na_xt, &na_o,
-                            &sa_vt, &sa_o, &glu, &dw, &emb})
+                            &sa_vt, &sa_o, &glu, &dw, &emb, &cur8})
       s += b->bytes();
     return s;
   }
@@ -189,7 +203,8 @@ struct zv_engine {
   bool defer_stores = false;       // A/B: ZV_GEMM_DEFER=1 lets the next tile's K loop run past the
                                    // plain bf16 linears' stores (bitwise equal; up to 6 % in isolation,
                                    // ~1 % slower in the model: profiles/r01_gemm_defer_ab.txt)
-  bool res_counted = true;         // A/B: ZV_RES_COUNTED=0 runs the residual linears through the
+  int res_counted = 31;            // A/B: ZV_RES_COUNTED=0 runs the residual linears through the
+                                   // (bit mask: 1 residual, 2 plain, 4 NA, 8 GLU, 16 transposed)
                                    // general epilogue (zv_gemm.inc gemm_epilogue)
   bool pair_resid = false;         // A/B: ZV_PAIR_RESID=1 carries the bf16-mode residual stream as a
                                    // bf16 hi/lo pair (8 B per update instead of 10): residual GEMMs
@@ -215,7 +230,7 @@ struct zv_engine {
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
-    res_counted = envi("ZV_RES_COUNTED", 1) != 0;
+    res_counted = envi("ZV_RES_COUNTED", 1) ? envi("ZV_RES_COUNTED_MASK", 31) : 0;
     resid_ws = envi("ZV_RESID_WS", 1);
     gemm_pp = envi("ZV_GEMM_PP", 0);
     gemm_dual = envi("ZV_GEMM_DUAL", 0);
@@ -301,7 +316,7 @@ struct zv_engine {
   }
   // perm (optional): row n of the device matrix is row perm[n] of the reference weight
   Linear make_linear(const std::string& prefix, int N, int K, bool bias, bool keep_f32,
-                     const std::vector<int>* perm = nullptr) {
+                     const std::vector<int>* perm = nullptr, bool fp8 = false) {
     Linear L;
     L.N = N; L.K = K;
     L.Npad = (int)round_up(N, W_NPAD);
@@ -320,6 +335,19 @@ struct zv_engine {
     L.lo = dalloc<bf16>(lo.size());
     ZV_CHECK(hipMemcpy(L.hi, hi.data(), hi.size() * sizeof(bf16), hipMemcpyHostToDevice));
     ZV_CHECK(hipMemcpy(L.lo, lo.data(), lo.size() * sizeof(bf16), hipMemcpyHostToDevice));
+    if (fp8 && cfg.precision == ZV_FP8 && K % MX8_KSTEP == 0) {
+      // MX-fp8 copy of the (permuted) fp32 weight, rows zero-padded to Npad
+      L.Kq = K;
+      std::vector<float> wp((size_t)L.Npad * K, 0.f);
+      for (int n = 0; n < N; ++n)
+        memcpy(&wp[(size_t)n * K], &w[(size_t)(perm ? (*perm)[n] : n) * K], (size_t)K * sizeof(float));
+      std::vector<uint8_t> q((size_t)L.Npad * K), sc((size_t)L.Npad * K / MX8_BLOCK);
+      mx8_quantize_host(wp.data(), K, L.Npad, K, q.data(), K, sc.data());
+      L.q8 = dalloc<uint8_t>(q.size());
+      L.s8 = dalloc<uint8_t>(sc.size());
+      ZV_CHECK(hipMemcpy(L.q8, q.data(), q.size(), hipMemcpyHostToDevice));
+      ZV_CHECK(hipMemcpy(L.s8, sc.data(), sc.size(), hipMemcpyHostToDevice));
+    }
     if (keep_f32) {
       L.w32 = dalloc<float>((size_t)N * K);
       ZV_CHECK(hipMemcpy(L.w32, w.data(), (size_t)N * K * sizeof(float), hipMemcpyHostToDevice));
@@ -369,7 +397,8 @@ struct zv_engine {
   void build_zipformer(ZipformerW& Z, const std::string& pre, int dim, int ff, int heads,
                        const std::vector<int>& ds, const std::vector<int>& layers,
                        const std::vector<int>& ks, std::vector<int> in_dims,
-                       std::vector<int> out_dims, bool two_stream, int temb_dim, bool guid) {
+                       std::vector<int> out_dims, bool two_stream, int temb_dim, bool guid,
+                       bool fp8_layers = false) {
     Z.dim = dim; Z.ff = ff; Z.heads = heads;
     Z.qd = cfg.query_head_dim; Z.pd = cfg.pos_head_dim; Z.vd = cfg.value_head_dim;
     Z.pos_dim = cfg.pos_dim; Z.temb_dim = temb_dim;
@@ -420,19 +449,19 @@ struct zv_engine {
         const int hs[3] = {ff * 3 / 4, ff, ff * 5 / 4};
         for (int f = 0; f < 3; ++f) {
           std::string fp = lp + "feed_forward" + std::to_string(f + 1) + ".";
-          W.ff_in[f] = make_linear(fp + "in_proj", hs[f], dim, true, false);
-          W.ff_out[f] = make_linear(fp + "out_proj", dim, hs[f], true, false);
+          W.ff_in[f] = make_linear(fp + "in_proj", hs[f], dim, true, false, nullptr, fp8_layers);
+          W.ff_out[f] = make_linear(fp + "out_proj", dim, hs[f], true, false, nullptr, fp8_layers);
         }
         const int hid = 3 * dim / 4;
         ZV_REQUIRE(hid % 16 == 0 && dim % 64 == 0, "encoder dim must be a multiple of 64");
         const std::vector<int> pna = perm_na(hid), pglu = perm_glu(dim);
         W.na_in = make_linear(lp + "nonlin_attention.in_proj", 3 * hid, dim, true, false, &pna);
-        W.na_out = make_linear(lp + "nonlin_attention.out_proj", dim, hid, true, false);
+        W.na_out = make_linear(lp + "nonlin_attention.out_proj", dim, hid, true, false, nullptr, fp8_layers);
         W.ks = ks[s];
         for (int c = 0; c < 2; ++c) {
           std::string cp = lp + "conv_module" + std::to_string(c + 1) + ".";
-          W.conv_in[c] = make_linear(cp + "in_proj", 2 * dim, dim, true, false, &pglu);
-          W.conv_out[c] = make_linear(cp + "out_proj", dim, dim, true, false);
+          W.conv_in[c] = make_linear(cp + "in_proj", 2 * dim, dim, true, false, &pglu, fp8_layers);
+          W.conv_out[c] = make_linear(cp + "out_proj", dim, dim, true, false, nullptr, fp8_layers);
           W.dw_w[c] = upload_f32(cp + "depthwise_conv.weight", (size_t)dim * W.ks);
           W.dw_b[c] = upload_f32(cp + "depthwise_conv.bias", dim);
         }
@@ -471,7 +500,7 @@ struct zv_engine {
     std::vector<int> out_dims = stereo() ? std::vector<int>{2 * F, F} : std::vector<int>{F};
     build_zipformer(dec, "fm_decoder.", cfg.fm_decoder_dim, cfg.fm_decoder_feedforward_dim,
                     cfg.fm_decoder_num_heads, ds, nl, ks, in_dims, out_dims, stereo(),
-                    cfg.time_embed_dim, distill());
+                    cfg.time_embed_dim, distill(), /*fp8_layers=*/true);
     build_zipformer(txt, "text_encoder.", cfg.text_encoder_dim, cfg.text_encoder_feedforward_dim,
                     cfg.text_encoder_num_heads, {1}, {cfg.text_encoder_num_layers},
                     {cfg.text_encoder_cnn_module_kernel}, {cfg.text_embed_dim}, {F}, false, -1,
@@ -540,8 +569,55 @@ struct zv_engine {
     return p;
   }
 
+  // ---------------------------------------------------------------- fp8 mode (ZV_FP8)
+  bool fp8_mode() const { return cfg.precision == ZV_FP8; }
+  // the MX-fp8 copy of a bf16 operand, for producers that do not write one themselves
+  void pack8(const Act& A, long M, int K, hipStream_t s) {
+    ZV_REQUIRE(A.h && A.q && K % MX8_BLOCK == 0 && A.ldq >= K && A.ld % 8 == 0, "fp8 pack: operand layout");
+    hipLaunchKernelGGL(zv_mx8_pack_kernel, grid1d(M * (K / 8)), dim3(256), 0, s, A.h, A.ld, M, K, A.q,
+                       A.ldq, A.qs);
+    ZV_LAUNCH_CHECK();
+  }
+  static GemmParams gp_linear8(const Linear& Lw, const Act& A, long M) {
+    GemmParams p = gp_linear(Lw, A, M);
+    p.Ah = reinterpret_cast<const bf16*>(A.q); p.Al = nullptr; p.lda = A.ldq;
+    p.As = A.qs; p.ldas = A.ldq / MX8_BLOCK;
+    p.Bh = reinterpret_cast<const bf16*>(Lw.q8); p.Bl = nullptr; p.ldb = Lw.Kq;
+    p.Bs = Lw.s8; p.ldbs = Lw.Kq / MX8_BLOCK;
+    return p;
+  }
+  // a linear on block-scaled fp8 MFMA (A and W MX-fp8): the counted epilogues, writing the
+  // output's fp8 copy where the next fp8 linear reads it (MXO 1: with the bf16 copy, 2: only)
+  void linear8(const Linear& Lw, const Act& A, long M, const Out& o, hipStream_t s) {
+    GemmParams p = gp_linear8(Lw, A, M);
+    p.act = o.act_fn;
+    p.C = o.C; p.ldc = o.ldc;
+    p.Ch = o.act.h; p.Cl = nullptr; p.ldch = o.act.ld;
+    p.resid = o.resid; p.orig = o.orig; p.byp = o.byp;
+    p.Cq = o.act.q; p.Cs = o.act.qs; p.ldcq = o.act.ldq;
+    ZV_REQUIRE(p.bias && !o.rowvec && !o.residh && Lw.N % 8 == 0, "fp8 linear: bias, no row vector");
+    const int mxo = o.act.q ? (o.act.h ? 1 : 2) : 0;
+    if (o.resid) {
+      ZV_REQUIRE(mxo != 2 && !o.act_fn, "fp8 residual linear: fp32 stream out");
+      const char* tag = "gemm_fp8_resid";
+      if (o.orig) {
+        if (mxo) launch_gemm<128, 128, 2, 2, 8, EPI_STD, 2, 2, MX8_KSTEP, 0, 0, 0, 2, 1>(p, 1, s, tag, true, gridx_resid);
+        else launch_gemm<128, 128, 2, 2, 8, EPI_STD, 2, 2, MX8_KSTEP, 0, 0, 0, 2, 0>(p, 1, s, tag, true, gridx_resid);
+      } else {
+        if (mxo) launch_gemm<128, 128, 2, 2, 8, EPI_STD, 2, 2, MX8_KSTEP, 0, 0, 0, 1, 1>(p, 1, s, tag, true, gridx_resid);
+        else launch_gemm<128, 128, 2, 2, 8, EPI_STD, 2, 2, MX8_KSTEP, 0, 0, 0, 1, 0>(p, 1, s, tag, true, gridx_resid);
+      }
+      return;
+    }
+    ZV_REQUIRE(!o.C && mxo, "fp8 plain linear: bias (+ activation) -> fp8 (+ bf16) copy");
+    if (mxo == 2) launch_gemm<128, 128, 2, 2, 8, EPI_STD, 2, 2, MX8_KSTEP, 0, 0, 0, 3, 2>(p, 1, s, "gemm_fp8", true, gridx_plain);
+    else launch_gemm<128, 128, 2, 2, 8, EPI_STD, 2, 2, MX8_KSTEP, 0, 0, 0, 3, 1>(p, 1, s, "gemm_fp8", true, gridx_plain);
+  }
+
   template <int SPLIT>
   void linear(const Linear& Lw, const Act& A, long M, const Out& o, hipStream_t s) {
+    if constexpr (SPLIT == 1)
+      if (Lw.q8 && A.q) { linear8(Lw, A, M, o, s); return; }
     GemmParams p = gp_linear(Lw, A, M);
     p.act = o.act_fn;
     p.C = o.C; p.ldc = o.ldc;
@@ -600,7 +676,7 @@ struct zv_engine {
         }
       // the counted residual epilogue (zv_gemm.inc gemm_epilogue_res; ROLE 2 = with the
       // bypass original) where its preconditions hold, else the general epilogue
-      const bool counted = res_counted && p.bias && !p.rowvec && !p.act && Lw.N % 8 == 0 &&
+      const bool counted = (res_counted & 1) && p.bias && !p.rowvec && !p.act && Lw.N % 8 == 0 &&
                            p.ldc % 4 == 0 && (!p.Ch || p.ldch % 8 == 0) && (!p.orig || p.byp) &&
                            (p.Cl != nullptr) == (SPLIT == 3 && p.Ch != nullptr);
       if (!counted) {
@@ -622,7 +698,7 @@ struct zv_engine {
       return;
     }
     // bias (+ activation) -> bf16 copy: the counted epilogue (ROLE 3)
-    const bool counted = res_counted && p.bias && p.Ch && !p.C && !p.rowvec && Lw.N % 8 == 0 &&
+    const bool counted = (res_counted & 2) && p.bias && p.Ch && !p.C && !p.rowvec && Lw.N % 8 == 0 &&
                          p.ldch % 8 == 0 && (p.Cl != nullptr) == (SPLIT == 3);
     if (counted) {
       if (occ_plain == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, tag, true, gridx_plain);
@@ -681,6 +757,16 @@ struct zv_engine {
         else launch_attn_stats<1>(fp, s);
       else launch_attn_stats<SPLIT>(fp, s);
     }
+    // fp8 mode: the working stream also carries an MX-fp8 copy (the A operand of the fp8
+    // feed-forward / convolution in-projections), written by the fp8 residual linears'
+    // epilogues and packed here where a bf16 producer (BiasNorm, the SelfAttention
+    // out-projection) wrote the stream last
+    const bool f8 = SPLIT == 1 && fp8_mode() && W.ff_in[0].q8 != nullptr;
+    if (f8) {
+      const Act c8 = ws.cur8.get(M, D, false, true, D, false);
+      cur_a.q = c8.q; cur_a.qs = c8.qs; cur_a.ldq = c8.ldq;
+      pack8(cur_a, M, D, s);
+    }
     Out res;                       // cur = cur + module(cur), with the hi/lo copy
     const bool pairm = SPLIT == 1 && pair_resid;
     if (pairm) {                   // the stream itself is the (hi, lo) pair
@@ -689,7 +775,8 @@ struct zv_engine {
       res.C = cur; res.ldc = D; res.resid = cur; res.act = cur_a;
     }
     auto ff = [&](int f, const Out& oe) {
-      Act hid = ws.hidden.get(M, W.ff_in[f].N, split);
+      // fp8: the SwooshL output only as the fp8 out-projection's operand
+      Act hid = ws.hidden.get(M, W.ff_in[f].N, split, f8, W.ff_in[f].N, !f8);
       Out o1; o1.act = hid; o1.act_fn = 1;          // SwooshL fused (scaling.py:1322-1334)
       linear<SPLIT>(W.ff_in[f], cur_a, M, o1, s);
       linear<SPLIT>(W.ff_out[f], hid, M, oe, s);
@@ -706,11 +793,11 @@ struct zv_engine {
       if constexpr (SPLIT == 1)
         if (gemm_pp && W.na_in.N % 192 == 0) { launch_gemm_pp<128, 192, 2, 4, EPI_NA, 0>(p, s, "gemm_bf16_na"); done = true; }
       if (done) {}
-      else if (res_counted && occ_fused == 2 && p.bias && W.na_in.N % 48 == 0 && p.ldch % 4 == 0)
+      else if ((res_counted & 4) && occ_fused == 2 && p.bias && W.na_in.N % 48 == 0 && p.ldch % 4 == 0)
         launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       else if (occ_fused == 2) launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       else launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 1>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
-      Act nao = ws.na_o.get(M, round_up(hid, 64), split);
+      Act nao = ws.na_o.get(M, round_up(hid, 64), split, f8, hid);
       if (materialize) {
         GemmParams q{};
         q.M = L; q.N = hid; q.K = L; q.nz2 = B; q.Brows = hid;
@@ -740,6 +827,7 @@ struct zv_engine {
         else if (hid <= 256) launch_attn_na<SPLIT, 2, QTILES>(f, s);
         else launch_attn_na<SPLIT, 3, QTILES>(f, s);
       }
+      if (f8) pack8(nao, M, hid, s);
       linear<SPLIT>(W.na_out, nao, M, res, s);
     }
     auto self_attn = [&](int a) {                     // SelfAttention (:564-570, :600-606)
@@ -749,7 +837,7 @@ struct zv_engine {
       GemmParams p = gp_linear(W.sa_in[a], cur_a, M);
       p.Cth = vt.h; p.Ctl = vt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)HV * Lpad;
       // N = 48: 64-row tiles give 2x the blocks of a 128-row grid (one tile column)
-      if (skinny_tiles && res_counted)
+      if (skinny_tiles && (res_counted & 16))
         launch_gemm<64, 64, 2, 2, SPLIT, EPI_TRANS, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, split ? "gemm_fp32_t" : "gemm_bf16_t", true, -1);
       else if (skinny_tiles) launch_gemm<64, 64, 2, 2, SPLIT, EPI_TRANS>(p, 1, s, split ? "gemm_fp32_t" : "gemm_bf16_t", true, -1);
       else launch_gemm<128, 64, 2, 2, SPLIT, EPI_TRANS>(p, 1, s, split ? "gemm_fp32_t" : "gemm_bf16_t");
@@ -781,21 +869,29 @@ struct zv_engine {
       Out e = res;
       if (temb) { e.rowvec = temb; e.rowvec_ld = D; e.rows_per_group = L; }
       linear<SPLIT>(W.sa_out[a], o, M, e, s);
+      if (f8) pack8(cur_a, M, D, s);                 // bf16 producer: refresh the fp8 copy
     };
     auto conv = [&](int c) {                          // ConvolutionModule (:1638-1680)
       Act g = ws.glu.get(M, D, split);
-      GemmParams p = gp_linear(W.conv_in[c], cur_a, M);
+      const bool c8 = f8 && W.conv_in[c].q8;
+      GemmParams p = c8 ? gp_linear8(W.conv_in[c], cur_a, M) : gp_linear(W.conv_in[c], cur_a, M);
       p.Ch = g.h; p.Cl = g.l; p.ldch = g.ld; p.rowmask = pad;
       bool done = false;
+      if (c8) {
+        ZV_REQUIRE(p.bias && W.conv_in[c].N % 32 == 0 && p.ldch % 8 == 0, "fp8 GLU linear layout");
+        launch_gemm<128, 128, 2, 2, 8, EPI_GLU, 2, 2, MX8_KSTEP, 0, 0, 0, 3>(p, 1, s, "gemm_fp8_glu", true, gridx_fused);
+        done = true;
+      }
       if constexpr (SPLIT == 1)
         if (gemm_pp && W.conv_in[c].N % 128 == 0) { launch_gemm_pp<128, 128, 2, 4, EPI_GLU, 0>(p, s, "gemm_bf16_glu"); done = true; }
       if (done) {}
-      else if (res_counted && occ_fused == 2 && p.bias && W.conv_in[c].N % 32 == 0 && p.ldch % 8 == 0)
+      else if ((res_counted & 8) && occ_fused == 2 && p.bias && W.conv_in[c].N % 32 == 0 && p.ldch % 8 == 0)
         launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       else if (occ_fused == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       else launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 1>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
-      Act dw = ws.dw.get(M, D, split);
+      Act dw = ws.dw.get(M, D, split, f8, D);
       launch_dwconv(g.h, g.l, g.ld, W.dw_w[c], W.dw_b[c], dw.h, dw.l, dw.ld, B, L, D, W.ks, s);
+      if (f8) pack8(dw, M, D, s);
       linear<SPLIT>(W.conv_out[c], dw, M, res, s);
     };
     self_attn(0);                                     // SA1 (+ temb)
@@ -930,7 +1026,7 @@ struct zv_engine {
   Act build_xin(Workspace& ws, const float* x, const float* tc, const float* sc, int B, int T,
                 int Fx, int copies, int zero_speech, hipStream_t s) {
     const int Ft = cfg.feat_dim, Fin = 2 * Fx + Ft;
-    const bool split = cfg.precision != ZV_BF16;     // fp32 / mixed: split input projection
+    const bool split = cfg.precision == ZV_FP32 || cfg.precision == ZV_MIXED;   // split input projection
     const long N = (long)copies * B;
     Act xin = ws.xin.get(N * T, round_up(Fin, 64), split);
     hipLaunchKernelGGL(zv_build_input_kernel, grid1d(N * T * Fin), dim3(256), 0, s, x, tc, sc,
@@ -1138,7 +1234,7 @@ struct zv_engine {
                    float* out, hipStream_t s) {
     const long n = (long)B * S;
     const int E = cfg.text_embed_dim;
-    const bool split = cfg.precision != ZV_BF16;     // mixed: the text encoder is split too
+    const bool split = cfg.precision == ZV_FP32 || cfg.precision == ZV_MIXED;   // mixed: the text encoder is split too
     io_split = false;
     Act emb = ws_txt.emb.get(n, round_up(E, 64), split);
     hipLaunchKernelGGL(zv_embed_kernel, grid1d(n * E), dim3(256), 0, s, tok, embed_table, emb.h,
@@ -1235,7 +1331,8 @@ zv_handle zv_create(const zv_config* cfg) {
     ZV_REQUIRE(cfg != nullptr, "null config");
     ZV_REQUIRE(cfg->num_stacks >= 1 && cfg->num_stacks <= ZV_MAX_STACKS, "bad num_stacks");
     ZV_REQUIRE(cfg->variant >= 0 && cfg->variant <= 3, "bad variant");
-    ZV_REQUIRE(cfg->precision == ZV_FP32 || cfg->precision == ZV_BF16 || cfg->precision == ZV_MIXED,
+    ZV_REQUIRE(cfg->precision == ZV_FP32 || cfg->precision == ZV_BF16 || cfg->precision == ZV_MIXED ||
+                   (cfg->precision == ZV_FP8 && std::string(ZV_OPERAND_NAME) == "bf16"),
                "bad precision");
     return new zv_engine(*cfg);
   } catch (const std::exception& e) {
@@ -1450,6 +1547,57 @@ static __global__ void zv_maxdiff_kernel(const float* a, const float* b, long n,
   }
   atomicMax(reinterpret_cast<int*>(out), __float_as_int(d));
   atomicMax(reinterpret_cast<int*>(out + 1), __float_as_int(r));
+}
+
+int zv_mx8_quantize(const float* x, int rows, int K, uint8_t* q, uint8_t* s) {
+  ZV_API_BEGIN
+  ZV_REQUIRE(x && q && s && rows >= 0 && K > 0, "bad arguments");
+  mx8_quantize_host(x, K, rows, K, q, round_up(K, MX8_KSTEP), s);
+  ZV_API_END
+}
+
+int zv_mx8_gemm_check(int M, int N, int K, const float* A, const float* W, float* C, uint8_t* Aq,
+                      uint8_t* As) {
+  ZV_API_BEGIN
+  ZV_REQUIRE(A && W && C && M > 0 && N > 0 && K > 0 && K % MX8_KSTEP == 0 && N % 8 == 0,
+             "zv_mx8_gemm_check: K a multiple of 128, N of 8");
+  hipStream_t s = nullptr;
+  const long Np = round_up(N, 128);
+  std::vector<bf16> ah((size_t)M * K);
+  for (size_t i = 0; i < ah.size(); ++i) ah[i] = (bf16)A[i];
+  std::vector<float> wp((size_t)Np * K, 0.f);
+  memcpy(wp.data(), W, (size_t)N * K * 4);
+  std::vector<uint8_t> wq((size_t)Np * K), ws((size_t)Np * K / MX8_BLOCK);
+  mx8_quantize_host(wp.data(), K, (int)Np, K, wq.data(), K, ws.data());
+  bf16* dA; uint8_t *dAq, *dAs, *dWq, *dWs; float *dC, *dB;
+  ZV_CHECK(hipMalloc(&dA, ah.size() * 2));
+  ZV_CHECK(hipMalloc(&dAq, (size_t)M * K));
+  ZV_CHECK(hipMalloc(&dAs, (size_t)M * K / MX8_BLOCK));
+  ZV_CHECK(hipMalloc(&dWq, wq.size()));
+  ZV_CHECK(hipMalloc(&dWs, ws.size()));
+  ZV_CHECK(hipMalloc(&dC, (size_t)M * N * 4));
+  ZV_CHECK(hipMalloc(&dB, (size_t)N * 4));
+  ZV_CHECK(hipMemcpy(dA, ah.data(), ah.size() * 2, hipMemcpyHostToDevice));
+  ZV_CHECK(hipMemcpy(dWq, wq.data(), wq.size(), hipMemcpyHostToDevice));
+  ZV_CHECK(hipMemcpy(dWs, ws.data(), ws.size(), hipMemcpyHostToDevice));
+  ZV_CHECK(hipMemset(dC, 0, (size_t)M * N * 4));
+  ZV_CHECK(hipMemset(dB, 0, (size_t)N * 4));
+  hipLaunchKernelGGL(zv_mx8_pack_kernel, grid1d((long)M * (K / 8)), dim3(256), 0, s, dA, (long)K, (long)M,
+                     K, dAq, (long)K, dAs);
+  ZV_LAUNCH_CHECK();
+  GemmParams p{};
+  p.M = M; p.N = N; p.K = K; p.nz2 = 1; p.Brows = (int)Np;
+  p.Ah = reinterpret_cast<const bf16*>(dAq); p.lda = K; p.As = dAs; p.ldas = K / MX8_BLOCK;
+  p.Bh = reinterpret_cast<const bf16*>(dWq); p.ldb = K; p.Bs = dWs; p.ldbs = K / MX8_BLOCK;
+  p.bias = dB; p.C = dC; p.ldc = N; p.resid = dC; p.rows_per_group = 1; p.rpb = 1;
+  launch_gemm<128, 128, 2, 2, 8, EPI_STD, 2, 2, MX8_KSTEP, 0, 0, 0, 1>(p, 1, s, "mx8_check", true, -1);
+  ZV_CHECK(hipDeviceSynchronize());
+  ZV_CHECK(hipMemcpy(C, dC, (size_t)M * N * 4, hipMemcpyDeviceToHost));
+  if (Aq) ZV_CHECK(hipMemcpy(Aq, dAq, (size_t)M * K, hipMemcpyDeviceToHost));
+  if (As) ZV_CHECK(hipMemcpy(As, dAs, (size_t)M * K / MX8_BLOCK, hipMemcpyDeviceToHost));
+  for (void* ptr : {(void*)dA, (void*)dAq, (void*)dAs, (void*)dWq, (void*)dWs, (void*)dC, (void*)dB})
+    ZV_CHECK(hipFree(ptr));
+  ZV_API_END
 }
 
 int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff, float* maxref) {

@@ -30,8 +30,10 @@ PRECISION_ID = {"fp32": 0, "bf16": 1}      # vocoder / BigVGAN precisions (main 
 # mode: fp16 MFMA operands in the decoder layers, split products for the decoder's input /
 # output projections, the attention-score projections and the text encoder (ZV_MIXED in the
 # fp16 library)
+# "fp8": the BASELINE C5 mode - the decoder layers' feed-forward, convolution-module and
+# NonlinAttention output linears on block-scaled MX-fp8 MFMA (ZV_FP8, main library)
 MODES = {"fp32": ("bf16", 0), "bf16": ("bf16", 1), "fp16": ("f16", 2),
-         "fp16_plain": ("f16", 1), "bf16_mixed": ("bf16", 2)}
+         "fp16_plain": ("f16", 1), "bf16_mixed": ("bf16", 2), "fp8": ("bf16", 3)}
 
 
 class ZvConfig(ctypes.Structure):
@@ -71,6 +73,8 @@ SIGNATURES = {
     "zv_bench_gemm": (_I, [_I, _I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_float)]),
     "zv_gemm_selftest": (_I, [_I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "zv_profile_report": (_I, [ctypes.c_char_p, _I]),
+    "zv_mx8_quantize": (_I, [_P, _I, _I, _P, _P]),
+    "zv_mx8_gemm_check": (_I, [_I, _I, _I, _P, _P, _P, _P, _P]),
     "zv_fm_decoder": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
     "zv_velocity": (_I, [_P, _F, _F, _P, _P, _P, _P, _I, _I, _P, _P]),
     "zv_euler_sample": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _F, _P]),
