@@ -138,3 +138,28 @@ def test_fp8_rows_independent_and_split_streams_bitwise(monkeypatch):
             assert d < 1e-5
         del m
     assert torch.equal(outs[0], outs[1])
+
+
+def test_fp8_fused_copies_equal_pack(monkeypatch):
+    """The bf16 producers that write the stream's / conv output's fp8 copy themselves
+    (ZV_FP8_FUSE bits: wave-specialised residual epilogue, depthwise conv, BiasNorm; DPP
+    cross-lane block max) are bitwise equal to running the pack kernel after them."""
+    rng = np.random.default_rng(6)
+    B, T = 2, 260
+    x = rng.standard_normal((B, T, 100), dtype=np.float32)
+    tc = rng.standard_normal((B, T, 100), dtype=np.float32)
+    sc = rng.standard_normal((B, T, 100), dtype=np.float32)
+    pm = np.arange(T)[None] >= np.array([T, 190])[:, None]
+    outs = []
+    for fuse in ("0", "7"):
+        monkeypatch.setenv("ZV_FP8_FUSE", fuse)
+        from zipvoice_amd.config import default_config
+        from zipvoice_amd.models import build_model
+        from zipvoice_amd.weights import synthetic_state_dict
+        cfg = default_config("zipvoice")
+        m = build_model(cfg, precision="fp8")
+        m.load_state_dict(synthetic_state_dict(cfg, 0))
+        m = m.to("cuda:0")
+        outs.append(m.engine.velocity(0.6, 1.0, cuda(x), cuda(tc), cuda(sc), cuda(pm)).cpu())
+        del m
+    assert torch.equal(outs[0], outs[1])

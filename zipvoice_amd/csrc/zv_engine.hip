@@ -193,6 +193,9 @@ struct zv_engine {
                                    // 0 = the 128x128 kernels (A/B arm, bitwise equal)
   int resid_ws = 1;                // residual linears on the wave-specialised epilogue kernel:
                                    // ZV_RESID_WS 1 = K <= 64 only (default), 2 = all, 0 = none
+  int fp8_fuse = 7;                // ZV_FP8_FUSE (fp8 mode): which bf16 producers write the fp8 copy
+                                   // themselves (1 wave-specialised residual epilogue, 2 depthwise
+                                   // conv, 4 BiasNorm); the others are followed by the pack kernel
   int sa_tp = 1;                   // ZV_SA_TP: 16-bit modes' SelfAttention with the positional
                                    // term on the MFMA chain (zv_attn_sa_tp_kernel), the head-0
                                    // stats / NonlinAttention scoring too; 0 = VALU forms
@@ -227,6 +230,7 @@ struct zv_engine {
     gridx_resid = envi("ZV_GEMM_GRIDX_RESID", -1);
     gridx_fused = envi("ZV_GEMM_GRIDX_FUSED", -1);
     sa_tp = envi("ZV_SA_TP", 1);
+    fp8_fuse = envi("ZV_FP8_FUSE", 7);
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
@@ -618,6 +622,14 @@ struct zv_engine {
   void linear(const Linear& Lw, const Act& A, long M, const Out& o, hipStream_t s) {
     if constexpr (SPLIT == 1)
       if (Lw.q8 && A.q) { linear8(Lw, A, M, o, s); return; }
+    // a 16-bit linear whose output also feeds an fp8 linear: its kernel writes the fp8 copy
+    // (wave-specialised residual epilogue) or the pack kernel does
+    if (!linear16<SPLIT>(Lw, A, M, o, s) && o.act.q) pack8(o.act, M, Lw.N, s);
+  }
+
+  // returns whether the kernel wrote the output's fp8 copy (o.act.q)
+  template <int SPLIT>
+  bool linear16(const Linear& Lw, const Act& A, long M, const Out& o, hipStream_t s) {
     GemmParams p = gp_linear(Lw, A, M);
     p.act = o.act_fn;
     p.C = o.C; p.ldc = o.ldc;
@@ -629,21 +641,21 @@ struct zv_engine {
       if (o.residh) {   // pair-residual linear: own instantiation, the residual policy
         if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 1>(p, 1, s, "gemm_bf16", true, gridx_resid);
         else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 1>(p, 1, s, "gemm_bf16", true, gridx_resid);
-        return;
+        return false;
       }
     }
     ZV_REQUIRE(!o.residh, "pair residual needs the bf16 mode");
     const char* tag = SPLIT == 3 ? "gemm_fp32" : "gemm_bf16";
     if (Lw.N <= 64) {   // own tag: the roofline's gemm_bf16 is the 128x128 instantiation alone
       launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD>(p, 1, s, SPLIT == 3 ? "gemm_fp32_n64" : "gemm_bf16_n64");
-      return;
+      return false;
     }
     if constexpr (SPLIT == 1) {
       if (gemm_pp && Lw.N % 128 == 0 && !o.act.l && !o.residh && A.ld % 8 == 0 &&
           (!o.C || o.ldc % 8 == 0) && (!o.act.h || o.act.ld % 8 == 0)) {
         if (o.resid) launch_gemm_pp<128, 128, 2, 4, EPI_STD, 1>(p, s, "gemm_bf16_resid");
         else launch_gemm_pp<128, 128, 2, 4, EPI_STD, 0>(p, s, "gemm_bf16");
-        return;
+        return false;
       }
     }
     if constexpr (SPLIT == 1) {
@@ -652,7 +664,7 @@ struct zv_engine {
       if (defer_stores && !o.resid && !o.C && o.act.h && !o.act.l && Lw.N % 128 == 0 &&
           o.act.ld % 8 == 0 && occ_plain == 2) {
         launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 8>(p, 1, s, tag, true, gridx_plain);
-        return;
+        return false;
       }
     }
     if (o.resid) {   // residual-stream linear: its own symbol / tag (HBM roofline)
@@ -662,7 +674,7 @@ struct zv_engine {
           GemmParams q = p;
           if (gemm_dual_ok(q)) {       // two phase-offset tile groups per CU (zv_gemm_dual.inc)
             launch_gemm_dual(q, s, "gemm_bf16_resid_dual");
-            return;
+            return false;
           }
         }
       if constexpr (SPLIT == 1)
@@ -671,8 +683,9 @@ struct zv_engine {
         // loses to zv_gemm_kernel's two co-resident blocks on longer K loops (+40 % at K = 1536,
         // profiles/r01_resid_ws_ab.txt)
         if (Lw.N % 128 == 0 && !o.act.l && (resid_ws == 2 || (resid_ws == 1 && Lw.K <= 64))) {
+          if (fp8_fuse & 1) { p.Cq = o.act.q; p.Cs = o.act.qs; p.ldcq = o.act.ldq; }
           launch_gemm_resid_ws(p, s, "gemm_bf16_resid_ws");   // own tag: one symbol per roofline tag
-          return;
+          return p.Cq != nullptr;
         }
       // the counted residual epilogue (zv_gemm.inc gemm_epilogue_res; ROLE 2 = with the
       // bypass original) where its preconditions hold, else the general epilogue
@@ -689,13 +702,13 @@ struct zv_engine {
         if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 1>(p, 1, s, rtag, true, gridx_resid);
         else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 1>(p, 1, s, rtag, true, gridx_resid);
       }
-      return;
+      return false;
     }
     // 96-wide tiles where they waste fewer columns than 128-wide ones (the attention-score
     // projection, N = 272: 288 computed columns instead of 384)
     if ((Lw.N + 95) / 96 * 96 < (Lw.N + 127) / 128 * 128) {
       launch_gemm<128, 96, 2, 2, SPLIT, EPI_STD, 2, 2>(p, 1, s, SPLIT == 3 ? "gemm_fp32_n96" : "gemm_bf16_n96", true, gridx_plain);
-      return;
+      return false;
     }
     // bias (+ activation) -> bf16 copy: the counted epilogue (ROLE 3)
     const bool counted = (res_counted & 2) && p.bias && p.Ch && !p.C && !p.rowvec && Lw.N % 8 == 0 &&
@@ -708,6 +721,7 @@ struct zv_engine {
     } else {
       launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1>(p, 1, s, tag, true, gridx_plain);
     }
+    return false;
   }
 
   // ---------------------------------------------------------------- one layer
@@ -717,7 +731,7 @@ struct zv_engine {
   template <int SPLIT>
   void layer(const ZipformerW& Z, const LayerW& W, Workspace& ws, float* src, Act src_a,
              float* cur, Act cur_a, int B, int L, const uint8_t* pad, const float* posP,
-             const float* temb, bool has_next, hipStream_t s) {
+             const float* temb, bool has_next, hipStream_t s, bool fresh8 = false) {
     const bool split = SPLIT == 3;
     const long M = (long)B * L;
     const int D = Z.dim, H = Z.heads;
@@ -758,14 +772,15 @@ struct zv_engine {
       else launch_attn_stats<SPLIT>(fp, s);
     }
     // fp8 mode: the working stream also carries an MX-fp8 copy (the A operand of the fp8
-    // feed-forward / convolution in-projections), written by the fp8 residual linears'
-    // epilogues and packed here where a bf16 producer (BiasNorm, the SelfAttention
-    // out-projection) wrote the stream last
+    // feed-forward / convolution in-projections), written by every producer of the stream:
+    // the residual linears' epilogues (fp8 and wave-specialised), the previous layer's
+    // BiasNorm (fresh8); packed here only at a stack's first layer
     const bool f8 = SPLIT == 1 && fp8_mode() && W.ff_in[0].q8 != nullptr;
+    Act c8;
     if (f8) {
-      const Act c8 = ws.cur8.get(M, D, false, true, D, false);
+      c8 = ws.cur8.get(M, D, false, true, D, false);
       cur_a.q = c8.q; cur_a.qs = c8.qs; cur_a.ldq = c8.ldq;
-      pack8(cur_a, M, D, s);
+      if (!fresh8 || !(fp8_fuse & 4)) pack8(cur_a, M, D, s);
     }
     Out res;                       // cur = cur + module(cur), with the hi/lo copy
     const bool pairm = SPLIT == 1 && pair_resid;
@@ -792,8 +807,10 @@ struct zv_engine {
       bool done = false;
       if constexpr (SPLIT == 1)
         if (gemm_pp && W.na_in.N % 192 == 0) { launch_gemm_pp<128, 192, 2, 4, EPI_NA, 0>(p, s, "gemm_bf16_na"); done = true; }
+      // counted NA epilogue: 16-bit modes (in the split mode it differs from the general one
+      // by up to 1.1e-4 in the decoder output, tools/counted_bisect.py; not bitwise: kept off)
       if (done) {}
-      else if ((res_counted & 4) && occ_fused == 2 && p.bias && W.na_in.N % 48 == 0 && p.ldch % 4 == 0)
+      else if ((res_counted & 4) && SPLIT == 1 && occ_fused == 2 && p.bias && W.na_in.N % 48 == 0 && p.ldch % 4 == 0)
         launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       else if (occ_fused == 2) launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       else launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 1>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
@@ -868,16 +885,15 @@ struct zv_engine {
       }
       Out e = res;
       if (temb) { e.rowvec = temb; e.rowvec_ld = D; e.rows_per_group = L; }
-      linear<SPLIT>(W.sa_out[a], o, M, e, s);
-      if (f8) pack8(cur_a, M, D, s);                 // bf16 producer: refresh the fp8 copy
+      linear<SPLIT>(W.sa_out[a], o, M, e, s);         // (+ the stream's fp8 copy)
     };
     auto conv = [&](int c) {                          // ConvolutionModule (:1638-1680)
       Act g = ws.glu.get(M, D, split);
-      const bool c8 = f8 && W.conv_in[c].q8;
-      GemmParams p = c8 ? gp_linear8(W.conv_in[c], cur_a, M) : gp_linear(W.conv_in[c], cur_a, M);
+      const bool g8 = f8 && W.conv_in[c].q8;
+      GemmParams p = g8 ? gp_linear8(W.conv_in[c], cur_a, M) : gp_linear(W.conv_in[c], cur_a, M);
       p.Ch = g.h; p.Cl = g.l; p.ldch = g.ld; p.rowmask = pad;
       bool done = false;
-      if (c8) {
+      if (g8) {
         ZV_REQUIRE(p.bias && W.conv_in[c].N % 32 == 0 && p.ldch % 8 == 0, "fp8 GLU linear layout");
         launch_gemm<128, 128, 2, 2, 8, EPI_GLU, 2, 2, MX8_KSTEP, 0, 0, 0, 3>(p, 1, s, "gemm_fp8_glu", true, gridx_fused);
         done = true;
@@ -890,8 +906,10 @@ struct zv_engine {
       else if (occ_fused == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       else launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 1>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       Act dw = ws.dw.get(M, D, split, f8, D);
-      launch_dwconv(g.h, g.l, g.ld, W.dw_w[c], W.dw_b[c], dw.h, dw.l, dw.ld, B, L, D, W.ks, s);
-      if (f8) pack8(dw, M, D, s);
+      const bool dq = f8 && (fp8_fuse & 2);
+      launch_dwconv(g.h, g.l, g.ld, W.dw_w[c], W.dw_b[c], dw.h, dw.l, dw.ld, B, L, D, W.ks, s,
+                    dq ? dw.q : nullptr, dw.qs, dw.ldq);
+      if (f8 && !dq) pack8(dw, M, D, s);
       linear<SPLIT>(W.conv_out[c], dw, M, res, s);
     };
     self_attn(0);                                     // SA1 (+ temb)
@@ -917,9 +935,13 @@ struct zv_engine {
                          has_next ? nullptr : src, src_a.h, src_a.l, has_next ? cur_a.h : nullptr,
                          has_next ? cur_a.l : nullptr, temb, L, M, D);
     } else {
+      // fp8: the next layer's working stream's fp8 copy as well (its fresh8)
+      const bool q2 = f8 && has_next && (fp8_fuse & 4);
+      ZV_REQUIRE(!q2 || D % 256 == 0, "fp8 BiasNorm copy: channels a multiple of 256");
       hipLaunchKernelGGL(zv_biasnorm_bypass_kernel, dim3(cdiv(M, 4)), dim3(256), 0, s, cur, src,
                          W.norm_bias, W.norm_log_scale, W.bypass, src, src_a.h, src_a.l,
-                         has_next ? cur : nullptr, cur_a.h, cur_a.l, (long)D, temb, L, M, D);
+                         has_next ? cur : nullptr, cur_a.h, cur_a.l, (long)D, temb, L, M, D,
+                         q2 ? c8.q : nullptr, q2 ? c8.qs : nullptr, q2 ? c8.ldq : 0L);
     }
     ZV_LAUNCH_CHECK();
   }
@@ -946,7 +968,7 @@ struct zv_engine {
     ZV_LAUNCH_CHECK();
     for (size_t li = 0; li < S.layers.size(); ++li)
       layer<SPLIT>(Z, S.layers[li], ws, src, src_a, cur, cur_a, B, L, pad,
-                   posP + li * (size_t)R * HPD, temb, li + 1 < S.layers.size(), s);
+                   posP + li * (size_t)R * HPD, temb, li + 1 < S.layers.size(), s, li > 0);
   }
 
   // ---------------------------------------------------------------- TTSZipformer
