@@ -52,6 +52,9 @@ struct LayerW {
   Linear ff_in[3], ff_out[3];
   Linear na_in, na_out;
   Linear conv_in[2], conv_out[2];
+  // bf16 mode: [conv_out[c] | sa_out[c]] concatenated along K (bias summed): one GEMM finishes
+  // both the SelfAttention and the convolution residual updates (zv_engine::layer)
+  Linear conv_sa_out[2];
   float* dw_w[2] = {nullptr, nullptr};
   float* dw_b[2] = {nullptr, nullptr};
   int ks = 0;
@@ -137,13 +140,15 @@ struct Workspace {
   // bf16 (hi/lo) GEMM operands
   ActBuf xin, main_a, dsrc_a, cur_a, qkp, W, hidden, na_y, na_xt, na_o, sa_vt, sa_o, glu, dw, emb;
   ActBuf cur8;   // fp8 mode: the working stream's MX-fp8 copy
+  ActBuf dwo;    // bf16 mode: [depthwise-conv output | SelfAttention output] (the K-concatenated
+                 // out-projection's operand)
   size_t bytes() const {
     size_t s = 0;
     for (const DBuf* b : {&main, &dsrc, &cur, &temb0, &temb1, &tstack, &tvec, &gvec, &posP, &mask2,
                           &maskds, &vout, &stats})
       s += b->bytes;
     for (const ActBuf* b : {&xin, &main_a, &dsrc_a, &cur_a, &qkp, &W, &hidden, &na_y, &na_xt, &na_o,
-                            &sa_vt, &sa_o, &glu, &dw, &emb, &cur8})
+                            &sa_vt, &sa_o, &glu, &dw, &emb, &cur8, &dwo})
       s += b->bytes();
     return s;
   }
@@ -193,6 +198,8 @@ struct zv_engine {
                                    // 0 = the 128x128 kernels (A/B arm, bitwise equal)
   int resid_ws = 1;                // residual linears on the wave-specialised epilogue kernel:
                                    // ZV_RESID_WS 1 = K <= 64 only (default), 2 = all, 0 = none
+  bool kcat_sa = true;             // ZV_KCAT_SA (bf16 mode): SelfAttention out-projection's fp32
+                                   // update folded into the conv out-projection (K concatenation)
   int fp8_fuse = 7;                // ZV_FP8_FUSE (fp8 mode): which bf16 producers write the fp8 copy
                                    // themselves (1 wave-specialised residual epilogue, 2 depthwise
                                    // conv, 4 BiasNorm); the others are followed by the pack kernel
@@ -231,6 +238,7 @@ struct zv_engine {
     gridx_fused = envi("ZV_GEMM_GRIDX_FUSED", -1);
     sa_tp = envi("ZV_SA_TP", 1);
     fp8_fuse = envi("ZV_FP8_FUSE", 7);
+    kcat_sa = envi("ZV_KCAT_SA", 1) != 0;
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
@@ -369,6 +377,35 @@ struct zv_engine {
     }
     return L;
   }
+  // [a | b] concatenated along K (a: N x Ka, b: N x Kb; bias a + b), rows padded like
+  // make_linear: the operand is [a's input (Ka columns) | b's input (Kb columns)]
+  Linear make_linear_kcat(const std::string& pa, int Ka, const std::string& pb, int Kb, int N) {
+    Linear L;
+    L.N = N; L.K = Ka + Kb;
+    L.Npad = (int)round_up(N, W_NPAD);
+    L.Kpad = (int)round_up(L.K, W_KPAD);
+    const auto& wa = take(pa + ".weight", (size_t)N * Ka);
+    const auto& wb = take(pb + ".weight", (size_t)N * Kb);
+    std::vector<bf16> hi((size_t)L.Npad * L.Kpad, (bf16)0.f), lo(hi.size(), (bf16)0.f);
+    for (int n = 0; n < N; ++n)
+      for (int k = 0; k < L.K; ++k) {
+        const float v = k < Ka ? wa[(size_t)n * Ka + k] : wb[(size_t)n * Kb + (k - Ka)];
+        const bf16 h = (bf16)v;
+        hi[(size_t)n * L.Kpad + k] = h;
+        lo[(size_t)n * L.Kpad + k] = (bf16)(v - (float)h);
+      }
+    L.hi = dalloc<bf16>(hi.size());
+    L.lo = dalloc<bf16>(lo.size());
+    ZV_CHECK(hipMemcpy(L.hi, hi.data(), hi.size() * sizeof(bf16), hipMemcpyHostToDevice));
+    ZV_CHECK(hipMemcpy(L.lo, lo.data(), lo.size() * sizeof(bf16), hipMemcpyHostToDevice));
+    const auto& ba = take(pa + ".bias", N);
+    const auto& bb = take(pb + ".bias", N);
+    std::vector<float> b(N);
+    for (int n = 0; n < N; ++n) b[n] = ba[n] + bb[n];
+    L.b = dalloc<float>(N);
+    ZV_CHECK(hipMemcpy(L.b, b.data(), N * sizeof(float), hipMemcpyHostToDevice));
+    return L;
+  }
   // NonlinAttention in_proj rows [s | x | y] -> groups of 48 = [s16 | x16 | y16]
   static std::vector<int> perm_na(int hid) {
     std::vector<int> p(3 * hid);
@@ -466,6 +503,10 @@ struct zv_engine {
           std::string cp = lp + "conv_module" + std::to_string(c + 1) + ".";
           W.conv_in[c] = make_linear(cp + "in_proj", 2 * dim, dim, true, false, &pglu, fp8_layers);
           W.conv_out[c] = make_linear(cp + "out_proj", dim, dim, true, false, nullptr, fp8_layers);
+          if (fp8_layers && cfg.precision == ZV_BF16)
+            W.conv_sa_out[c] = make_linear_kcat(cp + "out_proj", dim,
+                                                lp + "self_attn" + std::to_string(c + 1) + ".out_proj",
+                                                heads * Z.vd, dim);
           W.dw_w[c] = upload_f32(cp + "depthwise_conv.weight", (size_t)dim * W.ks);
           W.dw_b[c] = upload_f32(cp + "depthwise_conv.bias", dim);
         }
@@ -689,15 +730,18 @@ struct zv_engine {
         }
       // the counted residual epilogue (zv_gemm.inc gemm_epilogue_res; ROLE 2 = with the
       // bypass original) where its preconditions hold, else the general epilogue
-      const bool counted = (res_counted & 1) && p.bias && !p.rowvec && !p.act && Lw.N % 8 == 0 &&
-                           p.ldc % 4 == 0 && (!p.Ch || p.ldch % 8 == 0) && (!p.orig || p.byp) &&
-                           (p.Cl != nullptr) == (SPLIT == 3 && p.Ch != nullptr);
+      const bool counted = (res_counted & 1) && p.bias && !(p.rowvec && p.orig) && !p.act && p.C &&
+                           Lw.N % 8 == 0 && p.ldc % 4 == 0 && (!p.Ch || p.ldch % 8 == 0) &&
+                           (!p.orig || p.byp) && (p.Cl != nullptr) == (SPLIT == 3 && p.Ch != nullptr);
       if (!counted) {
         if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2>(p, 1, s, rtag, true, gridx_resid);
         else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1>(p, 1, s, rtag, true, gridx_resid);
       } else if (p.orig) {
         if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 2>(p, 1, s, rtag, true, gridx_resid);
         else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 2>(p, 1, s, rtag, true, gridx_resid);
+      } else if (p.rowvec) {         // + the row-group vector (ROLE 4)
+        if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 4>(p, 1, s, rtag, true, gridx_resid);
+        else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 4>(p, 1, s, rtag, true, gridx_resid);
       } else {
         if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 1>(p, 1, s, rtag, true, gridx_resid);
         else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 1>(p, 1, s, rtag, true, gridx_resid);
@@ -847,10 +891,19 @@ struct zv_engine {
       if (f8) pack8(nao, M, hid, s);
       linear<SPLIT>(W.na_out, nao, M, res, s);
     }
+    // bf16 mode: the SelfAttention output lands next to the depthwise-conv output ([dw | o],
+    // K = D + HV) and the convolution out-projection [conv_out | sa_out] finishes both residual
+    // updates in one GEMM; the SelfAttention out-projection itself only writes the bf16 copy of
+    // the stream the convolution module reads (cur + sa + temb: 6 B per element, not 10)
+    const bool kcat = SPLIT == 1 && kcat_sa && !f8 && !pairm && temb && W.conv_sa_out[0].hi &&
+                      !materialize;
+    Act dwo;
+    if (kcat) dwo = ws.dwo.get(M, round_up(W.conv_sa_out[0].K, 64), false);
     auto self_attn = [&](int a) {                     // SelfAttention (:564-570, :600-606)
       const int vd = Z.vd, HV = H * vd;
       Act vt = ws.sa_vt.get((long)B * HV, Lpad, split);
       Act o = ws.sa_o.get(M, 64, split);
+      if (kcat) { o = dwo; o.h += D; }               // columns [D, D + HV) of [dw | o]
       GemmParams p = gp_linear(W.sa_in[a], cur_a, M);
       p.Cth = vt.h; p.Ctl = vt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)HV * Lpad;
       // N = 48: 64-row tiles give 2x the blocks of a 128-row grid (one tile column)
@@ -885,6 +938,7 @@ struct zv_engine {
       }
       Out e = res;
       if (temb) { e.rowvec = temb; e.rowvec_ld = D; e.rows_per_group = L; }
+      if (kcat) e.C = nullptr;                        // fp32 update: the conv out-projection's
       linear<SPLIT>(W.sa_out[a], o, M, e, s);         // (+ the stream's fp8 copy)
     };
     auto conv = [&](int c) {                          // ConvolutionModule (:1638-1680)
@@ -905,12 +959,18 @@ struct zv_engine {
         launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       else if (occ_fused == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       else launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 1>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
-      Act dw = ws.dw.get(M, D, split, f8, D);
+      Act dw = kcat ? dwo : ws.dw.get(M, D, split, f8, D);
       const bool dq = f8 && (fp8_fuse & 2);
       launch_dwconv(g.h, g.l, g.ld, W.dw_w[c], W.dw_b[c], dw.h, dw.l, dw.ld, B, L, D, W.ks, s,
                     dq ? dw.q : nullptr, dw.qs, dw.ldq);
       if (f8 && !dq) pack8(dw, M, D, s);
-      linear<SPLIT>(W.conv_out[c], dw, M, res, s);
+      if (kcat) {                                     // cur += [dw | o] . [conv_out | sa_out]^T + temb
+        Out e = res;
+        e.rowvec = temb; e.rowvec_ld = D; e.rows_per_group = L;
+        linear<SPLIT>(W.conv_sa_out[c], dw, M, e, s);
+      } else {
+        linear<SPLIT>(W.conv_out[c], dw, M, res, s);
+      }
     };
     self_attn(0);                                     // SA1 (+ temb)
     conv(0);                                          // conv1
