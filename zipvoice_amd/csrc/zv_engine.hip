@@ -198,6 +198,8 @@ struct zv_engine {
                                    // 0 = the 128x128 kernels (A/B arm, bitwise equal)
   int resid_ws = 1;                // residual linears on the wave-specialised epilogue kernel:
                                    // ZV_RESID_WS 1 = K <= 64 only (default), 2 = all, 0 = none
+  bool ff1_src = true;             // ZV_FF1_SRC: FF1's residual read as src + temb (row vector) instead
+                                   // of a working stream BiasNorm / the stack entry wrote in fp32
   bool kcat_sa = true;             // ZV_KCAT_SA (bf16 mode): SelfAttention out-projection's fp32
                                    // update folded into the conv out-projection (K concatenation)
   int fp8_fuse = 7;                // ZV_FP8_FUSE (fp8 mode): which bf16 producers write the fp8 copy
@@ -239,6 +241,7 @@ struct zv_engine {
     sa_tp = envi("ZV_SA_TP", 1);
     fp8_fuse = envi("ZV_FP8_FUSE", 7);
     kcat_sa = envi("ZV_KCAT_SA", 1) != 0;
+    ff1_src = envi("ZV_FF1_SRC", 1) != 0;
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
@@ -639,13 +642,17 @@ struct zv_engine {
     p.C = o.C; p.ldc = o.ldc;
     p.Ch = o.act.h; p.Cl = nullptr; p.ldch = o.act.ld;
     p.resid = o.resid; p.orig = o.orig; p.byp = o.byp;
+    p.rowvec = o.rowvec; p.rowvec_ld = o.rowvec_ld; p.rows_per_group = o.rows_per_group;
     p.Cq = o.act.q; p.Cs = o.act.qs; p.ldcq = o.act.ldq;
-    ZV_REQUIRE(p.bias && !o.rowvec && !o.residh && Lw.N % 8 == 0, "fp8 linear: bias, no row vector");
+    ZV_REQUIRE(p.bias && !o.residh && Lw.N % 8 == 0 && (!o.rowvec || (o.resid && !o.orig && o.act.q)),
+               "fp8 linear: bias; a row vector only on a residual linear with the fp8 copy");
     const int mxo = o.act.q ? (o.act.h ? 1 : 2) : 0;
     if (o.resid) {
       ZV_REQUIRE(mxo != 2 && !o.act_fn, "fp8 residual linear: fp32 stream out");
       const char* tag = "gemm_fp8_resid";
-      if (o.orig) {
+      if (o.rowvec) {
+        launch_gemm<128, 128, 2, 2, 8, EPI_STD, 2, 2, MX8_KSTEP, 0, 0, 0, 4, 1>(p, 1, s, tag, true, gridx_resid);
+      } else if (o.orig) {
         if (mxo) launch_gemm<128, 128, 2, 2, 8, EPI_STD, 2, 2, MX8_KSTEP, 0, 0, 0, 2, 1>(p, 1, s, tag, true, gridx_resid);
         else launch_gemm<128, 128, 2, 2, 8, EPI_STD, 2, 2, MX8_KSTEP, 0, 0, 0, 2, 0>(p, 1, s, tag, true, gridx_resid);
       } else {
@@ -840,7 +847,17 @@ struct zv_engine {
       linear<SPLIT>(W.ff_in[f], cur_a, M, o1, s);
       linear<SPLIT>(W.ff_out[f], hid, M, oe, s);
     };
-    ff(0, res);                                       // FF1 (:536)
+    if (pairm || !ff1_src) {
+      ff(0, res);                                     // FF1 (:536)
+    } else {
+      // FF1's residual is the layer input + the time embedding (src + temb, what the working
+      // stream holds on entry): read from src with the row vector, so neither BiasNorm nor
+      // the stack entry writes the fp32 working stream (only its bf16 / fp8 copies)
+      Out e1 = res;
+      e1.resid = src;
+      if (temb) { e1.rowvec = temb; e1.rowvec_ld = D; e1.rows_per_group = L; }
+      ff(0, e1);
+    }
     {                                                 // NonlinAttention (:542-562)
       const int hid = W.na_in.N / 3;
       Act y = ws.na_y.get(M, hid, split);
@@ -1000,7 +1017,9 @@ struct zv_engine {
       ZV_REQUIRE(!q2 || D % 256 == 0, "fp8 BiasNorm copy: channels a multiple of 256");
       hipLaunchKernelGGL(zv_biasnorm_bypass_kernel, dim3(cdiv(M, 4)), dim3(256), 0, s, cur, src,
                          W.norm_bias, W.norm_log_scale, W.bypass, src, src_a.h, src_a.l,
-                         has_next ? cur : nullptr, cur_a.h, cur_a.l, (long)D, temb, L, M, D,
+                         ff1_src ? (float*)nullptr : cur, has_next ? cur_a.h : nullptr,
+                         has_next ? cur_a.l : nullptr,
+                         (long)D, temb, L, M, D,
                          q2 ? c8.q : nullptr, q2 ? c8.qs : nullptr, q2 ? c8.ldq : 0L);
     }
     ZV_LAUNCH_CHECK();
@@ -1015,8 +1034,10 @@ struct zv_engine {
     const bool pairm = SPLIT == 1 && pair_resid;
     float* cur = pairm ? nullptr : ws.cur.get<float>(M * Z.dim);
     Act cur_a = ws.cur_a.get(M, Z.dim, split || pairm);
-    hipLaunchKernelGGL(zv_stack_entry_kernel, grid1d(M * Z.dim), dim3(256), 0, s, src, temb, cur,
-                       src_a.h, src_a.l, cur_a.h, cur_a.l, (long)Z.dim, M, Z.dim, L);
+    // the fp32 working stream is not written here: the first layer's FF1 reads src + temb
+    hipLaunchKernelGGL(zv_stack_entry_kernel, grid1d(M * Z.dim), dim3(256), 0, s, src, temb,
+                       (pairm || ff1_src) ? nullptr : cur, src_a.h, src_a.l, cur_a.h, cur_a.l, (long)Z.dim, M,
+                       Z.dim, L);
     ZV_LAUNCH_CHECK();
     // positional encoding of length L and every layer's linear_pos projection of it, in one
     // launch into the workspace (zipformer.py:983-1056, :1239): no host table, no cache, no
