@@ -163,3 +163,34 @@ def test_fp8_fused_copies_equal_pack(monkeypatch):
         outs.append(m.engine.velocity(0.6, 1.0, cuda(x), cuda(tc), cuda(sc), cuda(pm)).cpu())
         del m
     assert torch.equal(outs[0], outs[1])
+
+
+def test_fp8_sample_graph_replay_and_oracle():
+    """The fp8 mode through the whole guided Euler solve (ZipVoice.solver.sample: the N-step
+    loop captured and replayed as one HIP graph): the replay equals the first (uncaptured)
+    run bitwise, a reserved workspace does not move, and the result stays within the mode's
+    tolerance of the oracle's Euler solve."""
+    from oracle.zipvoice_np import ZipVoiceOracle
+    from zipvoice_amd.config import default_config
+    from zipvoice_amd.weights import synthetic_state_dict
+    rng = np.random.default_rng(9)
+    B, T = 2, 180
+    x0 = rng.standard_normal((B, T, 100), dtype=np.float32)
+    tc = rng.standard_normal((B, T, 100), dtype=np.float32)
+    sc = (0.3 * rng.standard_normal((B, T, 100)) - 0.5).astype(np.float32)
+    pm = np.arange(T)[None] >= np.array([T, 131])[:, None]
+    m = model("zipvoice", "fp8")
+    m.engine.reserve(B, T)
+    before = m.engine.device_bytes()
+    args = dict(x=cuda(x0), text_condition=cuda(tc), speech_condition=cuda(sc),
+                padding_mask=cuda(pm), num_step=4, guidance_scale=1.0, t_shift=0.5)
+    first = m.solver.sample(**args).cpu()
+    again = m.solver.sample(**args).cpu()
+    torch.cuda.synchronize()
+    assert torch.equal(first, again)
+    assert m.engine.device_bytes() == before
+    cfg = default_config("zipvoice")
+    ref = ZipVoiceOracle(cfg, synthetic_state_dict(cfg, 0)).euler(x0, tc, sc, pm, 4, 1.0, t_shift=0.5)
+    err = np.abs(first.numpy() - ref)[~pm]
+    print(f"fp8 Euler 4 steps B={B} T={T}: mean={err.mean():.3e} max={err.max():.3e}")
+    assert err.mean() < TOL_FP8[0] and err.max() < TOL_FP8[1]
