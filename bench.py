@@ -61,9 +61,10 @@ HBM_PEAK_GBS = 8000.0
 # PMC traffic per launch (tools/pmc_traffic.py) of the two GEMM families the roofline
 # reports: the residual-stream linears (ROLE = 1) and the plain / activation linears
 # (newest measurement first)
-TRAFFIC_FILES = {"gemm_bf16_resid": ["r02b_gemm_resid_traffic.json", "r02_gemm_resid_traffic.json",
-                                     "r01_gemm_resid_traffic.json"],
-                 "gemm_bf16": ["r02b_gemm_traffic.json", "r02_gemm_traffic.json", "r01_gemm_traffic.json"]}
+TRAFFIC_FILES = {"gemm_bf16_resid": ["r02c_gemm_resid_traffic.json", "r02b_gemm_resid_traffic.json",
+                                     "r02_gemm_resid_traffic.json", "r01_gemm_resid_traffic.json"],
+                 "gemm_bf16": ["r02c_gemm_traffic.json", "r02b_gemm_traffic.json", "r02_gemm_traffic.json",
+                               "r01_gemm_traffic.json"]}
 # analytic FLOPs of one decoder sequence-forward (FlopCounterMode fit on the
 # reference, within 1 %) and of the vocoder per frame
 def decoder_flops(T):
