@@ -196,10 +196,15 @@ struct zv_engine {
   int gemm_pp = 0;                 // ZV_GEMM_PP: bf16 linears with N % 128 == 0 (and the GLU / NA
                                    // in-projections) on the ping-pong kernel (zv_gemm_pp.inc);
                                    // 0 = the 128x128 kernels (A/B arm, bitwise equal)
-  int resid_ws = 1;                // residual linears on the wave-specialised epilogue kernel:
-                                   // ZV_RESID_WS 1 = K <= 64 only (default), 2 = all, 0 = none
+  int resid_ws = 0;                // residual linears on the wave-specialised epilogue kernel:
+                                   // ZV_RESID_WS 1 = K <= 64 only, 2 = all, 0 = none (default: since the
+                                   // counted epilogue, zv_gemm_kernel is faster there too - fp8-mode SA
+                                   // out-projections 50.0 -> 28.7 ms per step, profiles/r02_fp8_ws_ab.txt)
   bool ff1_src = true;             // ZV_FF1_SRC: FF1's residual read as src + temb (row vector) instead
                                    // of a working stream BiasNorm / the stack entry wrote in fp32
+  bool sa_copy = true;             // ZV_SA_COPY: the copy-only SelfAttention out-projection on the
+                                   // counted epilogue (ROLE 5) instead of the wave-specialised kernel
+                                   // (bitwise equal; 36.3 -> 17.0 ms per step, profiles/r02_sa_copy_ab.txt)
   bool kcat_sa = true;             // ZV_KCAT_SA (bf16 mode): SelfAttention out-projection's fp32
                                    // update folded into the conv out-projection (K concatenation)
   int fp8_fuse = 7;                // ZV_FP8_FUSE (fp8 mode): which bf16 producers write the fp8 copy
@@ -241,12 +246,13 @@ struct zv_engine {
     sa_tp = envi("ZV_SA_TP", 1);
     fp8_fuse = envi("ZV_FP8_FUSE", 7);
     kcat_sa = envi("ZV_KCAT_SA", 1) != 0;
+    sa_copy = envi("ZV_SA_COPY", 1) != 0;
     ff1_src = envi("ZV_FF1_SRC", 1) != 0;
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
     res_counted = envi("ZV_RES_COUNTED", 1) ? envi("ZV_RES_COUNTED_MASK", 31) : 0;
-    resid_ws = envi("ZV_RESID_WS", 1);
+    resid_ws = envi("ZV_RESID_WS", 0);
     gemm_pp = envi("ZV_GEMM_PP", 0);
     gemm_dual = envi("ZV_GEMM_DUAL", 0);
     split_streams = envi("ZV_SPLIT_STREAMS", 3);
@@ -725,7 +731,14 @@ struct zv_engine {
             return false;
           }
         }
-      if constexpr (SPLIT == 1)
+      if constexpr (SPLIT == 1) {
+        // the copy-only form (no fp32 output) on the counted epilogue (A/B ZV_SA_COPY)
+        if (sa_copy && !p.C && p.rowvec && !p.orig && !o.act.l && !o.act.q && p.Ch && p.bias &&
+            Lw.N % 8 == 0 && p.ldch % 8 == 0) {
+          if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 5>(p, 1, s, "gemm_bf16_resid_copy", true, gridx_resid);
+          else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 5>(p, 1, s, "gemm_bf16_resid_copy", true, gridx_resid);
+          return false;
+        }
         // wave-specialised epilogue (zv_gemm_ws.inc): faster where the linear is all epilogue
         // (K <= 64: SelfAttention out-projections, -8 %); its single 4-wave MMA group per CU
         // loses to zv_gemm_kernel's two co-resident blocks on longer K loops (+40 % at K = 1536,
@@ -735,6 +748,7 @@ struct zv_engine {
           launch_gemm_resid_ws(p, s, "gemm_bf16_resid_ws");   // own tag: one symbol per roofline tag
           return p.Cq != nullptr;
         }
+      }
       // the counted residual epilogue (zv_gemm.inc gemm_epilogue_res; ROLE 2 = with the
       // bypass original) where its preconditions hold, else the general epilogue
       const bool counted = (res_counted & 1) && p.bias && !(p.rowvec && p.orig) && !p.act && p.C &&
@@ -747,6 +761,12 @@ struct zv_engine {
         if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 2>(p, 1, s, rtag, true, gridx_resid);
         else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 2>(p, 1, s, rtag, true, gridx_resid);
       } else if (p.rowvec) {         // + the row-group vector (ROLE 4)
+        if constexpr (SPLIT == 1)
+          if (o.act.q && o.act.h && p.Ch) {   // fp8 mode: + the stream's fp8 copy (MXO 1)
+            p.Cq = o.act.q; p.Cs = o.act.qs; p.ldcq = o.act.ldq;
+            launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 4, 1>(p, 1, s, rtag, true, gridx_resid);
+            return true;
+          }
         if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 4>(p, 1, s, rtag, true, gridx_resid);
         else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 4>(p, 1, s, rtag, true, gridx_resid);
       } else {
