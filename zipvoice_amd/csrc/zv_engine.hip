@@ -200,6 +200,7 @@ struct zv_engine {
                                    // ZV_RESID_WS 1 = K <= 64 only, 2 = all, 0 = none (default: since the
                                    // counted epilogue, zv_gemm_kernel is faster there too - fp8-mode SA
                                    // out-projections 50.0 -> 28.7 ms per step, profiles/r02_fp8_ws_ab.txt)
+  int n96_mode = 2;                // ZV_N96: the attention-score projection's tiles (see linear16)
   bool ff1_src = true;             // ZV_FF1_SRC: FF1's residual read as src + temb (row vector) instead
                                    // of a working stream BiasNorm / the stack entry wrote in fp32
   bool sa_copy = true;             // ZV_SA_COPY: the copy-only SelfAttention out-projection on the
@@ -247,6 +248,7 @@ struct zv_engine {
     fp8_fuse = envi("ZV_FP8_FUSE", 7);
     kcat_sa = envi("ZV_KCAT_SA", 1) != 0;
     sa_copy = envi("ZV_SA_COPY", 1) != 0;
+    n96_mode = envi("ZV_N96", 2);
     ff1_src = envi("ZV_FF1_SRC", 1) != 0;
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
@@ -778,6 +780,19 @@ struct zv_engine {
     // 96-wide tiles where they waste fewer columns than 128-wide ones (the attention-score
     // projection, N = 272: 288 computed columns instead of 384)
     if ((Lw.N + 95) / 96 * 96 < (Lw.N + 127) / 128 * 128) {
+      // ZV_N96: 2 (default) = 128x128 tiles on the counted plain epilogue (384 columns computed),
+      // 1 = 128x64 counted (320), 0 = 128x96 on the general epilogue (288): bitwise equal,
+      // 9.1 / 10.1 / 12.9 ms per step (profiles/r02_n96_counted_ab.txt)
+      const bool cnt = (res_counted & 2) && p.bias && p.Ch && !p.C && !p.resid && !p.rowvec && !p.act &&
+                       Lw.N % 8 == 0 && p.ldch % 8 == 0 && (p.Cl != nullptr) == (SPLIT == 3);
+      if (cnt && n96_mode == 1) {
+        launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, SPLIT == 3 ? "gemm_fp32_n96" : "gemm_bf16_n96", true, gridx_plain);
+        return false;
+      }
+      if (cnt && n96_mode == 2) {
+        launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, SPLIT == 3 ? "gemm_fp32_n96" : "gemm_bf16_n96", true, gridx_plain);
+        return false;
+      }
       launch_gemm<128, 96, 2, 2, SPLIT, EPI_STD, 2, 2>(p, 1, s, SPLIT == 3 ? "gemm_fp32_n96" : "gemm_bf16_n96", true, gridx_plain);
       return false;
     }
