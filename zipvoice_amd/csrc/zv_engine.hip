@@ -598,9 +598,17 @@ struct zv_engine {
   // ---------------------------------------------------------------- launch helpers
   void small_linear(const Linear& L, const float* in, int ldin, int M, float* out, int ldout,
                     int pre, const float* add, hipStream_t s) {
-    const long n = (long)M * L.N;
-    hipLaunchKernelGGL(zv_small_linear_kernel, dim3((unsigned)cdiv(n, 4L)), dim3(256), 0, s, in, ldin, L.w32,
-                       L.K, L.b, add, out, ldout, M, L.N, L.K, pre);
+    // one block per (row, 32 outputs) with the row's activation staged in LDS; the per-output
+    // kernel only where the row does not fit LDS
+    if (M > 0 && L.K <= 8192) {
+      hipLaunchKernelGGL(zv_small_linear_rows_kernel, dim3((unsigned)M, (unsigned)cdiv(L.N, SL_NB)), dim3(256),
+                         (size_t)L.K * sizeof(float), s,
+                         in, ldin, L.w32, L.K, L.b, add, out, ldout, M, L.N, L.K, pre);
+    } else {
+      const long n = (long)M * L.N;
+      hipLaunchKernelGGL(zv_small_linear_kernel, dim3((unsigned)cdiv(n, 4L)), dim3(256), 0, s, in, ldin, L.w32,
+                         L.K, L.b, add, out, ldout, M, L.N, L.K, pre);
+    }
     ZV_LAUNCH_CHECK();
   }
 
