@@ -1,4 +1,5 @@
 // Probe of the block-scaled fp8 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4) operand map on
+// build: hipcc --offload-arch=gfx950 -O2 tools/probe/mx8_probe.hip -o tools/probe/mx8_probe
 // gfx950.  Data: lane l (row l&15, c = l>>4) holds the 16-B chunks c and c + 4 of its 128-B
 // K row (bytes 0-15: K 16c .. 16c+15, bytes 16-31: K 64+16c ..), the same chunks as the
 // bf16 16x16x32 map over two K steps.  Scales: lane l supplies the E8M0 scale of K block c
