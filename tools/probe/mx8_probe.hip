@@ -1,11 +1,11 @@
 // Probe of the block-scaled fp8 MFMA (v_mfma_scale_f32_16x16x128_f8f6f4) operand map on
-// build: hipcc --offload-arch=gfx950 -O2 tools/probe/mx8_probe.hip -o tools/probe/mx8_probe
 // gfx950.  Data: lane l (row l&15, c = l>>4) holds the 16-B chunks c and c + 4 of its 128-B
 // K row (bytes 0-15: K 16c .. 16c+15, bytes 16-31: K 64+16c ..), the same chunks as the
 // bf16 16x16x32 map over two K steps.  Scales: lane l supplies the E8M0 scale of K block c
 // = K [32c, 32c+32) of row l&15 (not of the bytes it holds).  Compares the MFMA against a
 // host fp64 sum over random e4m3 bytes and random scales.  (A first hypothesis, lane l
 // holding K [32c, 32c+32) itself, measured max rel. error 1.2e2: tools/probe/mx8_probe2.hip.)
+// build: hipcc --offload-arch=gfx950 -O2 tools/probe/mx8_probe.hip -o tools/probe/mx8_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>

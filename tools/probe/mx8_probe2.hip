@@ -1,6 +1,6 @@
 // Diagnostic probe of v_mfma_scale_f32_16x16x128_f8f6f4 (fp8 e4m3 A and B): prints the
-// build: hipcc --offload-arch=gfx950 -O2 tools/probe/mx8_probe2.hip -o tools/probe/mx8_probe2
 // result of structured inputs so the lane maps of data and scales can be read off.
+// build: hipcc --offload-arch=gfx950 -O2 tools/probe/mx8_probe2.hip -o tools/probe/mx8_probe2
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
