@@ -123,6 +123,15 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
  * fp32 C; mode 0 plain, 1 SwooshL, 2 residual.  Writes max |diff| and max |ref|. */
 int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff, float* maxref);
 
+/* Attention plan (host only, no GPU; test infrastructure): the LDS bytes of the fused
+ * attention consumers a layer of sequence length L would launch — SelfAttention (sa_plo < 0:
+ * the plain kernel, 0 / 1: the Toeplitz kernel without / with the table's lo half),
+ * NonlinAttention of value width nv_na with scoring form tpm, the head-0 statistics — and
+ * whether the fused path is taken (fits = 1) or the W-materialising fallback (0).
+ * split: 1 (16-bit operands) or 3 (fp32-accurate hi/lo). */
+int zv_attn_plan(int split, int sa_plo, int tpm, int L, int nv_na, int64_t* lds_sa, int64_t* lds_na,
+                 int64_t* lds_stats, int* fits);
+
 /* MX-fp8 operand format of the fp8 mode (csrc/zv_mx8.inc): e4m3 values, one E8M0 scale byte per
  * 32 consecutive K elements.  zv_mx8_quantize: the host quantiser the engine applies to the
  * fp8 weights (host pointers, no GPU: x (rows, K) fp32 -> q (rows, ldq), s (rows, ldq / 32),

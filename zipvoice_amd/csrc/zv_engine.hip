@@ -18,6 +18,7 @@
 
 #include "zv_common.h"
 #include "zv_gemm.inc"
+#include "zv_gemm256.inc"
 #include "zv_gemm_ws.inc"
 #include "zv_gemm_dual.inc"
 #include "zv_gemm_pp.inc"
@@ -224,6 +225,10 @@ struct zv_engine {
   int res_counted = 31;            // A/B: ZV_RES_COUNTED=0 runs the residual linears through the
                                    // (bit mask: 1 residual, 2 plain, 4 NA, 8 GLU, 16 transposed)
                                    // general epilogue (zv_gemm.inc gemm_epilogue)
+  // ZV_GEMM256: the 256x256 phased kernel (zv_gemm256.inc) for the bias (+ SwooshL) and GLU
+  // linears with at least gemm256_min_tiles tiles (1 persistent, 2 one tile per block, 0 off)
+  int gemm256 = 1, gemm256_min_tiles = 256;
+  bool biasnorm_v = true;          // ZV_BIASNORM_V: BiasNorm with every row load up front
   bool pair_resid = false;         // A/B: ZV_PAIR_RESID=1 carries the bf16-mode residual stream as a
                                    // bf16 hi/lo pair (8 B per update instead of 10): residual GEMMs
                                    // -4..9 %, but the forward is unchanged (other kernels slower,
@@ -259,6 +264,18 @@ struct zv_engine {
     gemm_dual = envi("ZV_GEMM_DUAL", 0);
     split_streams = envi("ZV_SPLIT_STREAMS", 3);
     split_min_rows = envi("ZV_SPLIT_MIN_ROWS", 8192);
+    gemm256 = envi("ZV_GEMM256", 1);
+    gemm256_min_tiles = envi("ZV_GEMM256_MIN_TILES", 256);
+    biasnorm_v = envi("ZV_BIASNORM_V", 1) != 0;
+  }
+  // the 256x256 kernel's preconditions (16-bit operands: the lo halves the fp32-accurate mode
+  // keeps beside them are not read; padded K rows, the direct
+  // epilogues' activations) and enough tiles to fill the chip
+  bool use_gemm256(const GemmParams& p) const {
+    return gemm256 != 0 && !p.Cl && !p.As && p.N % 8 == 0 && (p.act == 0 || p.act == 1) &&
+           p.lda % 8 == 0 && p.ldb % 8 == 0 && p.lda >= round_up(p.K, GEMM_BK) &&
+           p.ldb >= round_up(p.K, GEMM_BK) && p.Brows >= p.N &&
+           (long)cdiv(p.M, 256) * cdiv(p.N, 256) >= gemm256_min_tiles;
   }
   // ---------------------------------------------------------------- HIP graphs
   // The whole N-step Euler solve (~250 launches per step) is captured once per
@@ -807,6 +824,11 @@ struct zv_engine {
     // bias (+ activation) -> bf16 copy: the counted epilogue (ROLE 3)
     const bool counted = (res_counted & 2) && p.bias && p.Ch && !p.C && !p.rowvec && Lw.N % 8 == 0 &&
                          p.ldch % 8 == 0 && (p.Cl != nullptr) == (SPLIT == 3);
+    if constexpr (SPLIT == 1)
+      if (counted && !o.act.q && use_gemm256(p)) {
+        launch_gemm256<EPI_STD, 3>(p, s, tag, gemm256 == 1);
+        return false;
+      }
     if (counted) {
       if (occ_plain == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, tag, true, gridx_plain);
       else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 3>(p, 1, s, tag, true, gridx_plain);
@@ -849,7 +871,8 @@ struct zv_engine {
     // attention: either materialise W (reference structure; A/B path, and the
     // fallback for lengths whose fused LDS images do not fit) or keep only
     // per-row softmax statistics and recompute scores inside each consumer
-    const bool materialize = materialize_attn || !fused_attn_fits<SPLIT>(L, W.na_in.N / 3);
+    const int sa_plo = (SPLIT == 1 && sa_tp) ? (io_split ? 1 : 0) : -1;
+    const bool materialize = materialize_attn || !fused_attn_fits<SPLIT>(L, W.na_in.N / 3, sa_plo, tp_na ? 1 : 0);
     Act Wt;
     FlashParams fp{};
     if (materialize) {
@@ -1014,6 +1037,11 @@ struct zv_engine {
       }
       if constexpr (SPLIT == 1)
         if (gemm_pp && W.conv_in[c].N % 128 == 0) { launch_gemm_pp<128, 128, 2, 4, EPI_GLU, 0>(p, s, "gemm_bf16_glu"); done = true; }
+      if constexpr (SPLIT == 1)
+        if (!done && (res_counted & 8) && p.bias && W.conv_in[c].N % 32 == 0 && p.ldch % 8 == 0 && use_gemm256(p)) {
+          launch_gemm256<EPI_GLU, 3>(p, s, "gemm_bf16_glu", gemm256 == 1);
+          done = true;
+        }
       if (done) {}
       else if ((res_counted & 8) && occ_fused == 2 && p.bias && W.conv_in[c].N % 32 == 0 && p.ldch % 8 == 0)
         launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
@@ -1058,12 +1086,19 @@ struct zv_engine {
       // fp8: the next layer's working stream's fp8 copy as well (its fresh8)
       const bool q2 = f8 && has_next && (fp8_fuse & 4);
       ZV_REQUIRE(!q2 || D % 256 == 0, "fp8 BiasNorm copy: channels a multiple of 256");
-      hipLaunchKernelGGL(zv_biasnorm_bypass_kernel, dim3(cdiv(M, 4)), dim3(256), 0, s, cur, src,
-                         W.norm_bias, W.norm_log_scale, W.bypass, src, src_a.h, src_a.l,
-                         ff1_src ? (float*)nullptr : cur, has_next ? cur_a.h : nullptr,
-                         has_next ? cur_a.l : nullptr,
-                         (long)D, temb, L, M, D,
-                         q2 ? c8.q : nullptr, q2 ? c8.qs : nullptr, q2 ? c8.ldq : 0L);
+      if (D == 512 && biasnorm_v)   // all loads of a row up front (ZV_BIASNORM_V=0: two-pass form)
+        hipLaunchKernelGGL(zv_biasnorm_bypass_v_kernel<2>, dim3(cdiv(M, 8)), dim3(512), 0, s, cur, src,
+                           W.norm_bias, W.norm_log_scale, W.bypass, src, src_a.h, src_a.l,
+                           ff1_src ? (float*)nullptr : cur, has_next ? cur_a.h : nullptr,
+                           has_next ? cur_a.l : nullptr, (long)D, temb, L, M,
+                           q2 ? c8.q : nullptr, q2 ? c8.qs : nullptr, q2 ? c8.ldq : 0L);
+      else
+        hipLaunchKernelGGL(zv_biasnorm_bypass_kernel, dim3(cdiv(M, 4)), dim3(256), 0, s, cur, src,
+                           W.norm_bias, W.norm_log_scale, W.bypass, src, src_a.h, src_a.l,
+                           ff1_src ? (float*)nullptr : cur, has_next ? cur_a.h : nullptr,
+                           has_next ? cur_a.l : nullptr,
+                           (long)D, temb, L, M, D,
+                           q2 ? c8.q : nullptr, q2 ? c8.qs : nullptr, q2 ? c8.ldq : 0L);
     }
     ZV_LAUNCH_CHECK();
   }
@@ -1693,6 +1728,20 @@ static __global__ void zv_maxdiff_kernel(const float* a, const float* b, long n,
   }
   atomicMax(reinterpret_cast<int*>(out), __float_as_int(d));
   atomicMax(reinterpret_cast<int*>(out + 1), __float_as_int(r));
+}
+
+int zv_attn_plan(int split, int sa_plo, int tpm, int L, int nv_na, int64_t* lds_sa, int64_t* lds_na,
+                 int64_t* lds_stats, int* fits) {
+  ZV_API_BEGIN
+  ZV_REQUIRE((split == 1 || split == 3) && L > 0 && nv_na > 0 && sa_plo >= -1 && sa_plo <= 1 &&
+                 tpm >= 0 && tpm <= 2 && (split == 1 || (sa_plo < 0 && tpm == 0)) && lds_sa && lds_na &&
+                 lds_stats && fits,
+             "bad arguments");
+  *lds_sa = (int64_t)(sa_plo < 0 ? sa_lds_bytes(L) : (sa_plo ? sa_tp_lds_bytes<1>(L) : sa_tp_lds_bytes<0>(L)));
+  *lds_na = (int64_t)(split == 1 ? na_lds_bytes_for<1>(L, nv_na, tpm) : na_lds_bytes_for<3>(L, nv_na, tpm));
+  *lds_stats = (int64_t)pos_mask_bytes(L, 64, true);
+  *fits = split == 1 ? fused_attn_fits<1>(L, nv_na, sa_plo, tpm) : fused_attn_fits<3>(L, nv_na, sa_plo, tpm);
+  ZV_API_END
 }
 
 int zv_mx8_quantize(const float* x, int rows, int K, uint8_t* q, uint8_t* s) {

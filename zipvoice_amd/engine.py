@@ -73,6 +73,7 @@ SIGNATURES = {
     "zv_bench_gemm": (_I, [_I, _I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_float)]),
     "zv_gemm_selftest": (_I, [_I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "zv_profile_report": (_I, [ctypes.c_char_p, _I]),
+    "zv_attn_plan": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "zv_mx8_quantize": (_I, [_P, _I, _I, _P, _P]),
     "zv_mx8_gemm_check": (_I, [_I, _I, _I, _P, _P, _P, _P, _P]),
     "zv_fm_decoder": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
