@@ -11,6 +11,15 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _needs_ab_build():
+    """A/B arm: its kernel is compiled only into the A/B build (build.py --out PATH
+    -DZV_AB_KERNELS, loaded with ZV_LIB_PATH=PATH); the product library skips this file."""
+    from zipvoice_amd import engine
+    if "ab_kernels" not in engine.load_library().zv_version().decode():
+        pytest.skip("A/B kernel not in the product build (build.py -DZV_AB_KERNELS)")
+
 torch = pytest.importorskip("torch")
 
 SHAPES = [(1000, 512, 1536), (78016, 512, 512), (4096, 512, 1920), (777, 256, 64),

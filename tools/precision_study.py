@@ -51,6 +51,10 @@ def q_fp16(x):
 
 
 QF = {"bf16": q_bf16, "fp16": q_fp16, None: lambda x: np.asarray(x, F32)}
+# one-sided formats of a linear's operands (the other side exact): "a16" rounds the activation
+# to fp16 and keeps the weight exact (the engine's weight-split product ah.bh + ah.bl), "w16" the
+# reverse (activation split: ah.bh + al.bh); outputs stored by the family round as fp16
+SIDE = {"a16": ("fp16", None), "w16": (None, "fp16")}
 
 
 class Emu:
@@ -62,7 +66,12 @@ class Emu:
         self.text_exact = False  # text encoder left in fp32
 
     def q(self, x, fam=None):
-        return QF[self.fam.get(fam or self.cur)](x)
+        f = self.fam.get(fam or self.cur)
+        return QF[SIDE[f][0] if f in SIDE else f](x)
+
+    def qw(self, w, fam=None):
+        f = self.fam.get(fam or self.cur)
+        return QF[SIDE[f][1] if f in SIDE else f](w)
 
 
 EMU = Emu({})
@@ -75,7 +84,7 @@ FP32_KEYS = ("time_emb", "time_embed", "guidance_scale_embed")   # fp32 small li
 def linear(x, w, b=None):
     if any(t in KEYS.get(id(w), "") for t in FP32_KEYS):
         return ORIG["linear"](x, w, b)
-    y = np.matmul(EMU.q(x), EMU.q(w).T)
+    y = np.matmul(EMU.q(x), EMU.qw(w).T)
     if b is not None:
         y = y + b
     return y.astype(F32)
@@ -192,6 +201,7 @@ def main():
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r02_precision_study.txt"))
     ap.add_argument("--fixture", default="sample_c1.npz")
     ap.add_argument("--mixed", action="store_true")
+    ap.add_argument("--r03", action="store_true")
     args = ap.parse_args()
     from zipvoice_amd.config import default_config
     from zipvoice_amd.weights import synthetic_state_dict
@@ -201,6 +211,18 @@ def main():
     o = Z.ZipVoiceOracle(cfg, synthetic_state_dict(cfg, 0))
     KEYS.update({id(v): k for k, v in o.sd.items()})
     fams = ["attn", "qk", "ff", "na", "sa", "conv", "io"]
+    if "--r03" in sys.argv:
+        # cheaper parity-grade candidates: one-sided split products for the attention-score
+        # projection, and dropping the text-encoder / in-out splits
+        base = {g: "fp16" for g in fams}
+        arms = [("io+attn fp32, rest fp16 +text fp32 (r02 mixed)", dict(base, io=None, attn=None), True),
+                ("io fp32, attn w16 (A split), +text fp32", dict(base, io=None, attn="w16"), True),
+                ("io fp32, attn a16 (W split), +text fp32", dict(base, io=None, attn="a16"), True),
+                ("io+attn fp32, text fp16", dict(base, io=None, attn=None), False),
+                ("attn fp32, io fp16, +text fp32", dict(base, attn=None), True),
+                ("io w16, attn w16, +text fp32", dict(base, io="w16", attn="w16"), True)]
+        run_arms(o, d, arms, args.out.replace(".txt", "_r03_" + args.fixture.replace(".npz", ".txt")))
+        return
     if "--mixed" in sys.argv:
         arms = []
         base = {g: "fp16" for g in fams}

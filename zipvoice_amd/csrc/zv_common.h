@@ -61,13 +61,15 @@ __device__ __forceinline__ float fast_ln(float x) {
   return __builtin_amdgcn_logf(x) * 0.693147180559945309f;
 }
 
-// SwooshLForward, scaling.py:1174-1180: log(1+exp(x-4)) (x-4 if inf) - 0.08x - 0.035
-// (exp overflows in fp32 for x-4 > 88.7; beyond 80 log(1+e^y) == y in fp32)
+// SwooshLForward, scaling.py:1174-1180: log(1+exp(x-4)) (x-4 if inf) - 0.08x - 0.035, in
+// base 2: t = log2(e) (x - 4); log(1 + e^(x-4)) = ln2 * max(log2(1 + 2^min(t, 126)), t) (the
+// max is exact past t ~ 24 and takes over where 2^t would overflow).  6 VALU + 2 transcendental
+// per element; every GEMM epilogue evaluates this one form, so a row's result does not depend
+// on which kernel (tile size) a batch size selects
 __device__ __forceinline__ float swoosh_l(float x) {
-  const float xo = x - 4.0f;
-  float ls = fast_ln(1.0f + fast_exp(xo));
-  ls = xo > 80.0f ? xo : ls;
-  return ls - 0.08f * x - 0.035f;
+  const float t = fmaf(x, 1.44269504088896341f, -5.77078016355585362f);
+  const float l = fmaxf(__builtin_amdgcn_logf(1.0f + __builtin_amdgcn_exp2f(fminf(t, 126.0f))), t);
+  return fmaf(l, 0.693147180559945309f, fmaf(x, -0.08f, -0.035f));
 }
 // SwooshRForward, scaling.py:1185-1191
 __device__ __forceinline__ float swoosh_r(float x) {

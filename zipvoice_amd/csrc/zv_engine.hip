@@ -19,9 +19,17 @@
 #include "zv_common.h"
 #include "zv_gemm.inc"
 #include "zv_gemm256.inc"
+// Rejected GEMM designs kept as measured A/B arms: compiled only into an A/B
+// build (build.py --out PATH -DZV_AB_KERNELS); the product library carries default-path
+// kernels only, and the environment switches that select them throw without it.
+#ifdef ZV_AB_KERNELS
 #include "zv_gemm_ws.inc"
 #include "zv_gemm_dual.inc"
 #include "zv_gemm_pp.inc"
+#define ZV_AB_TAG " ab_kernels"
+#else
+#define ZV_AB_TAG ""
+#endif
 #include "zv_attn.inc"
 #include "zv_elem.inc"
 #include "zv_flash.inc"
@@ -227,8 +235,14 @@ struct zv_engine {
                                    // general epilogue (zv_gemm.inc gemm_epilogue)
   // ZV_GEMM256: the 256x256 phased kernel (zv_gemm256.inc) for the bias (+ SwooshL) and GLU
   // linears with at least gemm256_min_tiles tiles (1 persistent, 2 one tile per block, 0 off)
-  int gemm256 = 1, gemm256_min_tiles = 256;
+  int gemm256 = 2, gemm256_min_tiles = 256;
   bool biasnorm_v = true;          // ZV_BIASNORM_V: BiasNorm with every row load up front
+  // mixed (fp16 parity) mode: the SelfAttention Toeplitz table's lo half (ZV_MIXED_PLO=1) and the
+  // fp32 positional table for the head-0 / NonlinAttention scoring (ZV_MIXED_TPNA=0).  Both off
+  // by default: the full-size velocity error is unchanged at C2-C5 (C5 8.6e-4 either way) and
+  // the step 18 ms shorter (profiles/r03_mixed_ab.txt)
+  bool mixed_plo = false, mixed_tpna = true;
+  bool mixed_wsplit = true;        // ZV_MIXED_WSPLIT: the attention-score projection weight-split (0: bf16x3)
   bool pair_resid = false;         // A/B: ZV_PAIR_RESID=1 carries the bf16-mode residual stream as a
                                    // bf16 hi/lo pair (8 B per update instead of 10): residual GEMMs
                                    // -4..9 %, but the forward is unchanged (other kernels slower,
@@ -262,11 +276,18 @@ struct zv_engine {
     resid_ws = envi("ZV_RESID_WS", 0);
     gemm_pp = envi("ZV_GEMM_PP", 0);
     gemm_dual = envi("ZV_GEMM_DUAL", 0);
+#ifndef ZV_AB_KERNELS
+    ZV_REQUIRE(!gemm_pp && !gemm_dual && !resid_ws,
+               "ZV_GEMM_PP / ZV_GEMM_DUAL / ZV_RESID_WS need the A/B build (build.py -DZV_AB_KERNELS)");
+#endif
     split_streams = envi("ZV_SPLIT_STREAMS", 3);
     split_min_rows = envi("ZV_SPLIT_MIN_ROWS", 8192);
-    gemm256 = envi("ZV_GEMM256", 1);
+    gemm256 = envi("ZV_GEMM256", 2);
     gemm256_min_tiles = envi("ZV_GEMM256_MIN_TILES", 256);
     biasnorm_v = envi("ZV_BIASNORM_V", 1) != 0;
+    mixed_plo = envi("ZV_MIXED_PLO", 0) != 0;
+    mixed_tpna = envi("ZV_MIXED_TPNA", 1) != 0;
+    mixed_wsplit = envi("ZV_MIXED_WSPLIT", 1) != 0;
   }
   // the 256x256 kernel's preconditions (16-bit operands: the lo halves the fp32-accurate mode
   // keeps beside them are not read; padded K rows, the direct
@@ -315,6 +336,8 @@ struct zv_engine {
     auto victim = graphs.begin();
     for (auto it = graphs.begin(); it != graphs.end(); ++it)
       if (it->second.last_use < victim->second.last_use) victim = it;
+    // its last replay may still run on gstream: destroy only after it drained
+    ZV_CHECK(hipStreamSynchronize(gstream));
     ZV_CHECK(hipGraphExecDestroy(victim->second.exec));
     graphs.erase(victim);
   }
@@ -531,7 +554,7 @@ struct zv_engine {
           std::string cp = lp + "conv_module" + std::to_string(c + 1) + ".";
           W.conv_in[c] = make_linear(cp + "in_proj", 2 * dim, dim, true, false, &pglu, fp8_layers);
           W.conv_out[c] = make_linear(cp + "out_proj", dim, dim, true, false, nullptr, fp8_layers);
-          if (fp8_layers && cfg.precision == ZV_BF16)
+          if (fp8_layers && (cfg.precision == ZV_BF16 || cfg.precision == ZV_MIXED))
             W.conv_sa_out[c] = make_linear_kcat(cp + "out_proj", dim,
                                                 lp + "self_attn" + std::to_string(c + 1) + ".out_proj",
                                                 heads * Z.vd, dim);
@@ -731,6 +754,7 @@ struct zv_engine {
       launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD>(p, 1, s, SPLIT == 3 ? "gemm_fp32_n64" : "gemm_bf16_n64");
       return false;
     }
+#ifdef ZV_AB_KERNELS
     if constexpr (SPLIT == 1) {
       if (gemm_pp && Lw.N % 128 == 0 && !o.act.l && !o.residh && A.ld % 8 == 0 &&
           (!o.C || o.ldc % 8 == 0) && (!o.act.h || o.act.ld % 8 == 0)) {
@@ -739,6 +763,7 @@ struct zv_engine {
         return false;
       }
     }
+#endif
     if constexpr (SPLIT == 1) {
       // bf16-only outputs on whole tiles: the next tile's K loop does not wait for
       // this tile's stores (counted vmcnt, zv_gemm.inc DEFER)
@@ -750,6 +775,7 @@ struct zv_engine {
     }
     if (o.resid) {   // residual-stream linear: its own symbol / tag (HBM roofline)
       const char* rtag = SPLIT == 3 ? "gemm_fp32_resid" : "gemm_bf16_resid";
+#ifdef ZV_AB_KERNELS
       if constexpr (SPLIT == 1)
         if (gemm_dual && !o.act.l && Lw.K >= 64) {
           GemmParams q = p;
@@ -758,6 +784,7 @@ struct zv_engine {
             return false;
           }
         }
+#endif
       if constexpr (SPLIT == 1) {
         // the copy-only form (no fp32 output) on the counted epilogue (A/B ZV_SA_COPY)
         if (sa_copy && !p.C && p.rowvec && !p.orig && !o.act.l && !o.act.q && p.Ch && p.bias &&
@@ -766,6 +793,7 @@ struct zv_engine {
           else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 5>(p, 1, s, "gemm_bf16_resid_copy", true, gridx_resid);
           return false;
         }
+#ifdef ZV_AB_KERNELS
         // wave-specialised epilogue (zv_gemm_ws.inc): faster where the linear is all epilogue
         // (K <= 64: SelfAttention out-projections, -8 %); its single 4-wave MMA group per CU
         // loses to zv_gemm_kernel's two co-resident blocks on longer K loops (+40 % at K = 1536,
@@ -775,6 +803,7 @@ struct zv_engine {
           launch_gemm_resid_ws(p, s, "gemm_bf16_resid_ws");   // own tag: one symbol per roofline tag
           return p.Cq != nullptr;
         }
+#endif
       }
       // the counted residual epilogue (zv_gemm.inc gemm_epilogue_res; ROLE 2 = with the
       // bypass original) where its preconditions hold, else the general epilogue
@@ -840,6 +869,22 @@ struct zv_engine {
     return false;
   }
 
+  // mixed mode's attention-score projection: the weight-split product a.(wh + wl) (SPLIT 2:
+  // the 16-bit layer input against the weight's hi/lo pair, 2 MFMAs per product instead of
+  // the bf16x3 form's 3).  tools/precision_study.py --r03: mean |err| 5.4e-4 / 8.8e-4 / 9.3e-4
+  // on the C1 / dialog / stereo fixtures vs 5.2e-4 / 8.6e-4 / 8.9e-4 fully split
+  // (profiles/r03_precision_study_r03_*.txt); 128x64 tiles (the hi/lo weight stage fits two
+  // blocks per CU)
+  void attn_in_wsplit(const Linear& Lw, const Act& A, long M, const Out& o, hipStream_t s) {
+    GemmParams p = gp_linear(Lw, A, M);
+    p.Al = nullptr;
+    p.Ch = o.act.h; p.Cl = nullptr; p.ldch = o.act.ld;
+    ZV_REQUIRE(p.bias && p.Ch && !o.act.l && !o.C && !o.resid && !o.act_fn && Lw.lo && Lw.N % 8 == 0 &&
+                   p.ldch % 8 == 0,
+               "weight-split projection: bias -> 16-bit copy");
+    launch_gemm<128, 64, 2, 2, 2, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, "gemm_wsplit_n96", true, gridx_plain);
+  }
+
   // ---------------------------------------------------------------- one layer
   // Zipformer2EncoderLayer.forward at inference (zipformer.py:489-642).
   // src/src_a: layer input (kept as src_orig, overwritten with the output);
@@ -861,17 +906,18 @@ struct zv_engine {
       // mixed mode: the attention-score projection as a split product (the layer input
       // src_a carries its lo half); q, k, p stay 16-bit
       Out o; o.act = qkp;
-      if (SPLIT == 1 && io_split) linear<3>(W.attn_in, src_a, M, o, s);
+      if (SPLIT == 1 && io_split && mixed_wsplit) attn_in_wsplit(W.attn_in, src_a, M, o, s);
+      else if (SPLIT == 1 && io_split) linear<3>(W.attn_in, src_a, M, o, s);
       else linear<SPLIT>(W.attn_in, src_a, M, o, s);
     }
     // head-0 scoring of the stats / NonlinAttention pair: Toeplitz MFMA form in bf16 mode
     // (mixed mode keeps the fp32 positional table there: its lo half would not fit the
     // NonlinAttention image at dialog lengths)
-    const bool tp_na = SPLIT == 1 && sa_tp && !io_split;
+    const bool tp_na = SPLIT == 1 && sa_tp && (!io_split || mixed_tpna);
     // attention: either materialise W (reference structure; A/B path, and the
     // fallback for lengths whose fused LDS images do not fit) or keep only
     // per-row softmax statistics and recompute scores inside each consumer
-    const int sa_plo = (SPLIT == 1 && sa_tp) ? (io_split ? 1 : 0) : -1;
+    const int sa_plo = (SPLIT == 1 && sa_tp) ? (io_split && mixed_plo ? 1 : 0) : -1;
     const bool materialize = materialize_attn || !fused_attn_fits<SPLIT>(L, W.na_in.N / 3, sa_plo, tp_na ? 1 : 0);
     Act Wt;
     FlashParams fp{};
@@ -907,8 +953,10 @@ struct zv_engine {
       res.C = cur; res.ldc = D; res.resid = cur; res.act = cur_a;
     }
     auto ff = [&](int f, const Out& oe) {
-      // fp8: the SwooshL output only as the fp8 out-projection's operand
-      Act hid = ws.hidden.get(M, W.ff_in[f].N, split, f8, W.ff_in[f].N, !f8);
+      // fp8: the SwooshL output only as the fp8 out-projection's operand (decided per in/out
+      // pair: a 16-bit out-projection reads the bf16 hidden copy)
+      const bool f8f = f8 && W.ff_in[f].q8 && W.ff_out[f].q8;
+      Act hid = ws.hidden.get(M, W.ff_in[f].N, split, f8f, W.ff_in[f].N, !f8f);
       Out o1; o1.act = hid; o1.act_fn = 1;          // SwooshL fused (scaling.py:1322-1334)
       linear<SPLIT>(W.ff_in[f], cur_a, M, o1, s);
       linear<SPLIT>(W.ff_out[f], hid, M, oe, s);
@@ -932,8 +980,10 @@ struct zv_engine {
       p.Ch = y.h; p.Cl = y.l; p.ldch = y.ld;
       p.Cth = xt.h; p.Ctl = xt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)hid * Lpad;
       bool done = false;
+#ifdef ZV_AB_KERNELS
       if constexpr (SPLIT == 1)
         if (gemm_pp && W.na_in.N % 192 == 0) { launch_gemm_pp<128, 192, 2, 4, EPI_NA, 0>(p, s, "gemm_bf16_na"); done = true; }
+#endif
       // counted NA epilogue: 16-bit modes (in the split mode it differs from the general one
       // by up to 1.1e-4 in the decoder output, tools/counted_bisect.py; not bitwise: kept off)
       if (done) {}
@@ -1011,9 +1061,9 @@ struct zv_engine {
         if constexpr (SPLIT == 1)
           if (sa_tp) {                   // positional term as a Toeplitz MFMA product
             if (sa_tp == 3) {          // A/B: the compiler's one-wave register budget
-              if (io_split) launch_attn_sa_tp<1, 1>(f, s);
+              if (io_split && mixed_plo) launch_attn_sa_tp<1, 1>(f, s);
               else launch_attn_sa_tp<0, 1>(f, s);
-            } else if (io_split) launch_attn_sa_tp<1>(f, s);
+            } else if (io_split && mixed_plo) launch_attn_sa_tp<1>(f, s);
             else launch_attn_sa_tp<0>(f, s);
             done = true;
           }
@@ -1035,8 +1085,10 @@ struct zv_engine {
         launch_gemm<128, 128, 2, 2, 8, EPI_GLU, 2, 2, MX8_KSTEP, 0, 0, 0, 3>(p, 1, s, "gemm_fp8_glu", true, gridx_fused);
         done = true;
       }
+#ifdef ZV_AB_KERNELS
       if constexpr (SPLIT == 1)
         if (gemm_pp && W.conv_in[c].N % 128 == 0) { launch_gemm_pp<128, 128, 2, 4, EPI_GLU, 0>(p, s, "gemm_bf16_glu"); done = true; }
+#endif
       if constexpr (SPLIT == 1)
         if (!done && (res_counted & 8) && p.bias && W.conv_in[c].N % 32 == 0 && p.ldch % 8 == 0 && use_gemm256(p)) {
           launch_gemm256<EPI_GLU, 3>(p, s, "gemm_bf16_glu", gemm256 == 1);
@@ -1481,6 +1533,7 @@ static float bench_variant(GemmParams p, int iters, bool persistent, hipStream_t
   return ms / iters;
 }
 
+#ifdef ZV_AB_KERNELS
 template <int BM, int BN, int WGM, int WGN, int EPI, int STAGES = 2>
 static float bench_variant_pp(GemmParams p, int iters, hipStream_t s) {
   hipEvent_t e0, e1;
@@ -1495,6 +1548,7 @@ static float bench_variant_pp(GemmParams p, int iters, hipStream_t s) {
   ZV_CHECK(hipEventDestroy(e0)); ZV_CHECK(hipEventDestroy(e1));
   return ms / iters;
 }
+#endif
 
 
 extern "C" {
@@ -1504,7 +1558,7 @@ const char* zv_last_error(void) { return g_last_error.c_str(); }
 #define ZV_SRC_HASH "unknown"
 #endif
 const char* zv_version(void) {
-  return "zipvoice_hip 0.2 (gfx950, " ZV_OPERAND_NAME " operands) src=" ZV_SRC_HASH;
+  return "zipvoice_hip 0.3 (gfx950, " ZV_OPERAND_NAME " operands" ZV_AB_TAG ") src=" ZV_SRC_HASH;
 }
 
 zv_handle zv_create(const zv_config* cfg) {
@@ -1670,9 +1724,11 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
     case 31: ms = bench_variant<128, 128, 2, 2, 3, 32>(p, iters, persistent, s); break;
     case 32: ms = bench_variant<256, 128, 2, 2, 2, 32>(p, iters, persistent, s); break;
     case 33: ms = bench_variant<256, 128, 2, 2, 3, 32>(p, iters, persistent, s); break;
+#ifdef ZV_AB_KERNELS
     case 50: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD>(p, iters, s); break;
     case 52: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD, 3>(p, iters, s); break;   // out mode 4 only
     case 53: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD, 4>(p, iters, s); break;   // out mode 4 only
+#endif
     case 72: {                     // counted plain epilogue (out mode 7)
       if (out_mode != 7) throw std::invalid_argument("variant 72: mode 7 only");
       ms = bench_variant<128, 128, 2, 2, 2, GEMM_BK, 0, 3>(p, iters, persistent, s);
@@ -1684,6 +1740,7 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
                          : bench_variant<128, 128, 2, 2, 2, GEMM_BK, 0, 2>(p, iters, persistent, s);
       break;
     }
+#ifdef ZV_AB_KERNELS
     case 60: {                     // dual-group residual kernel (out mode 2 only)
       if (out_mode != 2) throw std::invalid_argument("variant 60: residual mode only");
       hipEvent_t e0, e1;
@@ -1698,6 +1755,7 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
       ZV_CHECK(hipEventDestroy(e0)); ZV_CHECK(hipEventDestroy(e1));
       break;
     }
+#endif
     default: throw std::invalid_argument("unknown variant");
   }
   *ms_out = ms;
@@ -1854,8 +1912,10 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
     else switch (variant) {
       case 30: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 4, 2, 32>(p, 1, s, "t", true, 0); break;
       case 40: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2, GEMM_BK, 8>(p, 1, s, "t", true, 0); break;
+#ifdef ZV_AB_KERNELS
       case 50: launch_gemm_pp<128, 128, 2, 4, EPI_STD, 0>(p, s, "t"); break;
       case 60: case 61: launch_gemm_dual(p, s, "t"); break;
+#endif
       // the counted residual epilogue (ROLE 1 / 2) against the general one
       case 70: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 1>(p, 1, s, "t", true, -1); break;
       case 71: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 2>(p, 1, s, "t", true, -1); break;
