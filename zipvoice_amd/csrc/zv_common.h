@@ -20,6 +20,7 @@ typedef _Float16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 bf16x2 __attribute__((ext_vector_type(2)));
 #define ZV_MFMA_16x16x32 __builtin_amdgcn_mfma_f32_16x16x32_f16
+#define ZV_MFMA_32x32x16 __builtin_amdgcn_mfma_f32_32x32x16_f16
 #define ZV_OPERAND_NAME "fp16"
 #else
 typedef __bf16 bf16;
@@ -27,9 +28,11 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 #define ZV_MFMA_16x16x32 __builtin_amdgcn_mfma_f32_16x16x32_bf16
+#define ZV_MFMA_32x32x16 __builtin_amdgcn_mfma_f32_32x32x16_bf16
 #define ZV_OPERAND_NAME "bf16"
 #endif
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define ZV_CHECK(expr)                                                                  \
   do {                                                                                  \

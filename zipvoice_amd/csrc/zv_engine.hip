@@ -19,6 +19,7 @@
 #include "zv_common.h"
 #include "zv_gemm.inc"
 #include "zv_gemm256.inc"
+#include "zv_ffn.inc"
 // Rejected GEMM designs kept as measured A/B arms: compiled only into an A/B
 // build (build.py --out PATH -DZV_AB_KERNELS); the product library carries default-path
 // kernels only, and the environment switches that select them throw without it.
@@ -59,6 +60,10 @@ struct LayerW {
   float* pos_w = nullptr;   // (H*pd, pos_dim)
   Linear sa_in[2], sa_out[2];
   Linear ff_in[3], ff_out[3];
+  // the fused FeedForward kernel's fragment-major copies of ff_in / ff_out (zv_ffn.inc; decoder
+  // layers of width 512 with hidden widths a multiple of 64, 16-bit modes)
+  bf16* ffn_w1f[3] = {nullptr, nullptr, nullptr};
+  bf16* ffn_w2f[3] = {nullptr, nullptr, nullptr};
   Linear na_in, na_out;
   Linear conv_in[2], conv_out[2];
   // bf16 mode: [conv_out[c] | sa_out[c]] concatenated along K (bias summed): one GEMM finishes
@@ -210,6 +215,10 @@ struct zv_engine {
                                    // counted epilogue, zv_gemm_kernel is faster there too - fp8-mode SA
                                    // out-projections 50.0 -> 28.7 ms per step, profiles/r02_fp8_ws_ab.txt)
   int n96_mode = 2;                // ZV_N96: the attention-score projection's tiles (see linear16)
+  // ZV_FFN: the decoder FeedForward modules as one fused kernel each (zv_ffn.inc: in_proj ->
+  // SwooshL -> out_proj -> residual without the hidden tensor in HBM) for at least ffn_min_rows rows
+  int ffn_fused = 0;
+  long ffn_min_rows = 0;
   bool ff1_src = true;             // ZV_FF1_SRC: FF1's residual read as src + temb (row vector) instead
                                    // of a working stream BiasNorm / the stack entry wrote in fp32
   bool sa_copy = true;             // ZV_SA_COPY: the copy-only SelfAttention out-projection on the
@@ -269,6 +278,8 @@ struct zv_engine {
     sa_copy = envi("ZV_SA_COPY", 1) != 0;
     n96_mode = envi("ZV_N96", 2);
     ff1_src = envi("ZV_FF1_SRC", 1) != 0;
+    ffn_fused = envi("ZV_FFN", 0);
+    ffn_min_rows = envi("ZV_FFN_MIN_ROWS", 0);
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
@@ -543,6 +554,18 @@ struct zv_engine {
           std::string fp = lp + "feed_forward" + std::to_string(f + 1) + ".";
           W.ff_in[f] = make_linear(fp + "in_proj", hs[f], dim, true, false, nullptr, fp8_layers);
           W.ff_out[f] = make_linear(fp + "out_proj", dim, hs[f], true, false, nullptr, fp8_layers);
+          if (fp8_layers && dim == FFN_D && hs[f] % (2 * FFN_HC) == 0 &&
+              (cfg.precision == ZV_BF16 || cfg.precision == ZV_MIXED)) {
+            const long n = (long)hs[f] * FFN_D;
+            W.ffn_w1f[f] = dalloc<bf16>(n);
+            W.ffn_w2f[f] = dalloc<bf16>(n);
+            hipLaunchKernelGGL(zv_ffn_pack_w1_kernel, dim3(cdiv(n, 256)), dim3(256), 0, 0, W.ff_in[f].hi,
+                               (long)W.ff_in[f].Kpad, hs[f], W.ffn_w1f[f]);
+            hipLaunchKernelGGL(zv_ffn_pack_w2_kernel, dim3(cdiv(n, 256)), dim3(256), 0, 0, W.ff_out[f].hi,
+                               (long)W.ff_out[f].Kpad, hs[f], W.ffn_w2f[f]);
+            ZV_LAUNCH_CHECK();
+            ZV_CHECK(hipDeviceSynchronize());
+          }
         }
         const int hid = 3 * dim / 4;
         ZV_REQUIRE(hid % 16 == 0 && dim % 64 == 0, "encoder dim must be a multiple of 64");
@@ -953,6 +976,20 @@ struct zv_engine {
       res.C = cur; res.ldc = D; res.resid = cur; res.act = cur_a;
     }
     auto ff = [&](int f, const Out& oe) {
+      if constexpr (SPLIT == 1) {
+        if (ffn_fused && W.ffn_w1f[f] && !pairm && !(f8 && W.ff_in[f].q8) && oe.C && oe.resid &&
+            !oe.act.l && !oe.residh && M >= ffn_min_rows && cur_a.ld % 8 == 0) {
+          FfnParams q{};
+          q.M = (int)M; q.H = W.ff_in[f].N;
+          q.X = cur_a.h; q.ldx = cur_a.ld;
+          q.W1f = W.ffn_w1f[f]; q.b1 = W.ff_in[f].b; q.W2f = W.ffn_w2f[f]; q.b2 = W.ff_out[f].b;
+          q.resid = oe.resid; q.C = oe.C; q.ldc = oe.ldc; q.Ch = oe.act.h; q.ldch = oe.act.ld;
+          q.rowvec = oe.rowvec; q.rowvec_ld = oe.rowvec_ld; q.rows_per_group = oe.rows_per_group;
+          q.orig = oe.orig; q.byp = oe.byp;
+          launch_ffn(q, s, "ffn_bf16");
+          return;
+        }
+      }
       // fp8: the SwooshL output only as the fp8 out-projection's operand (decided per in/out
       // pair: a 16-bit out-projection reads the bf16 hidden copy)
       const bool f8f = f8 && W.ff_in[f].q8 && W.ff_out[f].q8;
