@@ -216,7 +216,8 @@ struct zv_engine {
                                    // out-projections 50.0 -> 28.7 ms per step, profiles/r02_fp8_ws_ab.txt)
   int n96_mode = 2;                // ZV_N96: the attention-score projection's tiles (see linear16)
   // ZV_FFN: the decoder FeedForward modules as one fused kernel each (zv_ffn.inc: in_proj ->
-  // SwooshL -> out_proj -> residual without the hidden tensor in HBM) for at least ffn_min_rows rows
+  // SwooshL -> out_proj -> residual without the hidden tensor in HBM) for at least ffn_min_rows
+  // rows; 2: FF3 also carries the layer's BiasNorm + bypass in its epilogue
   int ffn_fused = 0;
   long ffn_min_rows = 0;
   bool ff1_src = true;             // ZV_FF1_SRC: FF1's residual read as src + temb (row vector) instead
@@ -554,7 +555,7 @@ struct zv_engine {
           std::string fp = lp + "feed_forward" + std::to_string(f + 1) + ".";
           W.ff_in[f] = make_linear(fp + "in_proj", hs[f], dim, true, false, nullptr, fp8_layers);
           W.ff_out[f] = make_linear(fp + "out_proj", dim, hs[f], true, false, nullptr, fp8_layers);
-          if (fp8_layers && dim == FFN_D && hs[f] % (2 * FFN_HC) == 0 &&
+          if (ffn_fused && fp8_layers && dim == FFN_D && hs[f] % (2 * FFN_HC) == 0 &&
               (cfg.precision == ZV_BF16 || cfg.precision == ZV_MIXED)) {
             const long n = (long)hs[f] * FFN_D;
             W.ffn_w1f[f] = dalloc<bf16>(n);
@@ -1159,13 +1160,30 @@ struct zv_engine {
     }
     self_attn(1);                                     // SA2 (+ temb)
     conv(1);                                          // conv2
-    {                                                 // FF3: only the fp32 stream feeds BiasNorm
+    // FF3 + BiasNorm + bypass in the fused FeedForward kernel's norm epilogue (the FF3 output
+    // never reaches HBM; zv_ffn.inc)
+    const bool ffn_norm = SPLIT == 1 && ffn_fused >= 2 && W.ffn_w1f[2] && !pairm && !f8 && D == FFN_D &&
+                          M >= ffn_min_rows && cur_a.ld == src_a.ld && cur_a.ld % 8 == 0;
+    if (ffn_norm) {
+      FfnParams q{};
+      q.M = (int)M; q.H = W.ff_in[2].N;
+      q.X = cur_a.h; q.ldx = cur_a.ld;
+      q.W1f = W.ffn_w1f[2]; q.b1 = W.ff_in[2].b; q.W2f = W.ffn_w2f[2]; q.b2 = W.ff_out[2].b;
+      q.resid = cur; q.orig = src; q.C = src; q.ldc = D;
+      q.Ch = src_a.h; q.Cl = src_a.l; q.ldch = src_a.ld;
+      q.byp = W.bypass; q.nb = W.norm_bias; q.log_scale = W.norm_log_scale;
+      q.rowvec = temb; q.rowvec_ld = D; q.rows_per_group = L;
+      q.C2h = has_next ? cur_a.h : nullptr; q.C2l = has_next ? cur_a.l : nullptr;
+      q.C2 = (has_next && !ff1_src) ? cur : nullptr;
+      launch_ffn(q, s, "ffn_norm_bf16");
+    } else {                                          // FF3: only the fp32 stream feeds BiasNorm
       Out e = res;                                    // (which rewrites both copies): no bf16 copy
       if (!pairm) e.act = Act{};
       ff(2, e);
     }
     // BiasNorm + bypass -> src; next layer's working copy (src + temb) -> cur
-    if (pairm) {   // pair stream; fp32 output only for the stack's last layer (next stack's input)
+    if (ffn_norm) {
+    } else if (pairm) {   // pair stream; fp32 output only for the stack's last layer (next stack's input)
       ZV_REQUIRE(D % 8 == 0 && cur_a.ld == src_a.ld, "pair-residual BiasNorm layout");
       hipLaunchKernelGGL(zv_biasnorm_bypass_pair_kernel, dim3(cdiv(M, 4)), dim3(256), 0, s, cur_a.h,
                          cur_a.l, src_a.h, src_a.l, src_a.ld, W.norm_bias, W.norm_log_scale, W.bypass,
