@@ -58,13 +58,15 @@ CONFIGS = {
 BF16_DENSE_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16
 FP32_MFMA_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
-# PMC traffic per launch (tools/pmc_traffic.py) of the two GEMM families the roofline
-# reports: the residual-stream linears (ROLE = 1) and the plain / activation linears
-# (newest measurement first)
-TRAFFIC_FILES = {"gemm_bf16_resid": ["r02c_gemm_resid_traffic.json", "r02b_gemm_resid_traffic.json",
-                                     "r02_gemm_resid_traffic.json", "r01_gemm_resid_traffic.json"],
-                 "gemm_bf16": ["r02c_gemm_traffic.json", "r02b_gemm_traffic.json", "r02_gemm_traffic.json",
-                               "r01_gemm_traffic.json"]}
+# PMC traffic per launch (tools/pmc_traffic.py) of the kernels the roofline reports, keyed by
+# the engine's profiler tag (one symbol per tag since round 3: the residual linears by ROLE, the
+# fused FeedForward with / without the BiasNorm epilogue); newest measurement first
+TRAFFIC_FILES = {"gemm_bf16_resid": ["r03_gemm_resid_r1_traffic.json", "r02c_gemm_resid_traffic.json"],
+                 "gemm_bf16_resid_rv": ["r03_gemm_resid_r4_traffic.json"],
+                 "gemm_bf16_resid_byp": ["r03_gemm_resid_r2_traffic.json"],
+                 "ffn_bf16": ["r03_ffn_traffic.json"],
+                 "ffn_norm_bf16": ["r03_ffn_norm_traffic.json"],
+                 "gemm_bf16": ["r03_gemm_traffic.json", "r02c_gemm_traffic.json", "r02b_gemm_traffic.json"]}
 # analytic FLOPs of one decoder sequence-forward (FlopCounterMode fit on the
 # reference, within 1 %) and of the vocoder per frame
 def decoder_flops(T):
@@ -172,7 +174,7 @@ def _kernel_roofline(name, r, total_ms):
     below the bf16 ridge point (<= ~250 FLOP/B vs 2500 TF/s / 8 TB/s = 312): bound HBM,
     achieved = algorithmic bytes per launch / average launch duration.  The others are
     priced on the dense MFMA peak of their dtype."""
-    hbm = name.endswith("_resid")
+    hbm = "_resid" in name
     sec = r["ms"] * 1e-3
     if hbm:
         achieved, peak, unit = r["bytes"] / sec / 1e9, HBM_PEAK_GBS, "GB/s"

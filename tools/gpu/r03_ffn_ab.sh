@@ -11,4 +11,4 @@ grep -E 'ZV_FFN|PASS|passed|fp16' $O/pytest_ffn.log | tail -12
 ZV_FFN=2 timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -q \
   --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
-bash tools/gpu/ab_env.sh ffnab ${1:-2} "ZV_FFN=0 ZV_DWCONV_PIPE=0" "ZV_FFN=0" "ZV_FFN=1" "ZV_FFN=2"
+bash tools/gpu/ab_env.sh ffnab ${1:-2} "ZV_FFN=0" "ZV_FFN=0 ZV_DWCONV_PIPE=1" "ZV_FFN=1 ZV_DWCONV_PIPE=1" "ZV_FFN=2 ZV_DWCONV_PIPE=1"

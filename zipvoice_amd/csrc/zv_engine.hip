@@ -798,7 +798,7 @@ struct zv_engine {
       }
     }
     if (o.resid) {   // residual-stream linear: its own symbol / tag (HBM roofline)
-      const char* rtag = SPLIT == 3 ? "gemm_fp32_resid" : "gemm_bf16_resid";
+      const char* rtag = SPLIT == 3 ? "gemm_fp32_resid" : "gemm_bf16_resid";   // ROLE 1
 #ifdef ZV_AB_KERNELS
       if constexpr (SPLIT == 1)
         if (gemm_dual && !o.act.l && Lw.K >= 64) {
@@ -837,10 +837,12 @@ struct zv_engine {
       if (!counted) {
         if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2>(p, 1, s, rtag, true, gridx_resid);
         else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1>(p, 1, s, rtag, true, gridx_resid);
-      } else if (p.orig) {
-        if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 2>(p, 1, s, rtag, true, gridx_resid);
-        else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 2>(p, 1, s, rtag, true, gridx_resid);
+      } else if (p.orig) {           // one tag per ROLE: the roofline's bytes and PMC traffic per symbol
+        const char* t2 = SPLIT == 3 ? "gemm_fp32_resid_byp" : "gemm_bf16_resid_byp";
+        if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 2>(p, 1, s, t2, true, gridx_resid);
+        else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 2>(p, 1, s, t2, true, gridx_resid);
       } else if (p.rowvec) {         // + the row-group vector (ROLE 4)
+        rtag = SPLIT == 3 ? "gemm_fp32_resid_rv" : "gemm_bf16_resid_rv";
         if constexpr (SPLIT == 1)
           if (o.act.q && o.act.h && p.Ch) {   // fp8 mode: + the stream's fp8 copy (MXO 1)
             p.Cq = o.act.q; p.Cs = o.act.qs; p.ldcq = o.act.ldq;
