@@ -217,8 +217,9 @@ struct zv_engine {
   int n96_mode = 2;                // ZV_N96: the attention-score projection's tiles (see linear16)
   // ZV_FFN: the decoder FeedForward modules as one fused kernel each (zv_ffn.inc: in_proj ->
   // SwooshL -> out_proj -> residual without the hidden tensor in HBM) for at least ffn_min_rows
-  // rows; 2: FF3 also carries the layer's BiasNorm + bypass in its epilogue
-  int ffn_fused = 0;
+  // rows; 2 (default): FF3 also carries the layer's BiasNorm + bypass in its epilogue.  C2 bench
+  // 445 -> 431 ms per step with the pipelined depthwise conv (profiles/r03_ffn_ab.txt)
+  int ffn_fused = 2;
   long ffn_min_rows = 0;
   bool ff1_src = true;             // ZV_FF1_SRC: FF1's residual read as src + temb (row vector) instead
                                    // of a working stream BiasNorm / the stack entry wrote in fp32
@@ -279,7 +280,7 @@ struct zv_engine {
     sa_copy = envi("ZV_SA_COPY", 1) != 0;
     n96_mode = envi("ZV_N96", 2);
     ff1_src = envi("ZV_FF1_SRC", 1) != 0;
-    ffn_fused = envi("ZV_FFN", 0);
+    ffn_fused = envi("ZV_FFN", 2);
     ffn_min_rows = envi("ZV_FFN_MIN_ROWS", 0);
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
