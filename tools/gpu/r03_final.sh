@@ -1,0 +1,38 @@
+#!/bin/bash
+# Round-3 validation + measurement of the current tree: every GPU test, smoke, PMC traffic per
+# roofline tag (FETCH_SIZE / WRITE_SIZE in separate passes), the bench line (reads that traffic),
+# a rocprofv3 kernel trace + stats of a short bench run, and the timed-schedule account (3 streams).
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+O=gpurun_out/final; mkdir -p $O
+step() { echo "== $1 $(date +%T)"; }
+step pytest
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+tail -2 $O/pytest_gpu.log
+step smoke
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+step pmc
+RX='zv_gemm_kernel|zv_ffn_kernel'
+timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -f csv --kernel-include-regex "$RX" -d $O/pmc_fetch -o run -- python3 tools/profile_forward.py --iters 1 > $O/pmc_fetch.log 2>&1 || { tail -5 $O/pmc_fetch.log; exit 1; }
+timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -f csv --kernel-include-regex "$RX" -d $O/pmc_write -o run -- python3 tools/profile_forward.py --iters 1 > $O/pmc_write.log 2>&1 || { tail -5 $O/pmc_write.log; exit 1; }
+F=$(ls $O/pmc_fetch/*counter_collection.csv | head -1); W=$(ls $O/pmc_write/*counter_collection.csv | head -1)
+for kv in "r03_gemm_resid_r1:zv_gemm_kernel<128, 128, 2, 2, 1, 0, 2, 2, 64, 0, 0, 0, 1, 1, 0>" \
+          "r03_gemm_resid_r4:zv_gemm_kernel<128, 128, 2, 2, 1, 0, 2, 2, 64, 0, 0, 0, 4, 1, 0>" \
+          "r03_gemm_resid_r2:zv_gemm_kernel<128, 128, 2, 2, 1, 0, 2, 2, 64, 0, 0, 0, 2, 1, 0>" \
+          "r03_ffn:zv_ffn_kernel<(true|false), (true|false), true, 0, false>" \
+          "r03_ffn_norm:zv_ffn_kernel<false, false, true, 0, true>" \
+          "r03_gemm:zv_gemm_kernel<128, 128, 2, 2, 1, 0, 2, 2, 64, 0, 0, 0, 3, 1, 0>"; do
+  n=${kv%%:*}; rx=${kv#*:}
+  python3 tools/pmc_traffic.py "$F" "$W" "$rx" profiles/${n}_traffic.json >> $O/pmc_traffic.log 2>&1
+done
+cat $O/pmc_traffic.log | cut -c1-200
+step bench
+timeout -k 10 500 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/bench.json'));print(d['ms_per_step'],d['value'],d['roofline']['kernel'],d['roofline']['frac']);print({k:v['ms_per_step'] for k,v in d.items() if isinstance(v,dict) and 'ms_per_step' in v})"
+step rocprof
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/rp -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-fp32-mode > $O/rp_bench.log 2>&1 || { tail -5 $O/rp_bench.log; exit 1; }
+step trace
+bash tools/gpu/r03_trace.sh final_trace - > $O/trace.log 2>&1 || { tail -5 $O/trace.log; exit 1; }
+tail -20 $O/trace.log
+step done

@@ -17,6 +17,7 @@ import re
 from collections import defaultdict
 
 CLASSES = [
+    ("ffn_fused", re.compile(r"zv_ffn_kernel")),
     ("gemm256_plain/glu", re.compile(r"zv_gemm256_kernel")),
     ("gemm_resid", re.compile(r"zv_gemm_kernel<.*, [1245], \d+, \d+>\(")),
     ("gemm_na", re.compile(r"zv_gemm_kernel<128, 96, 2, 2, 1, 2,")),
