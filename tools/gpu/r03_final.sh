@@ -24,7 +24,7 @@ for kv in "r03_gemm_resid_r1:zv_gemm_kernel<128, 128, 2, 2, 1, 0, 2, 2, 64, 0, 0
           "r03_ffn_norm:zv_ffn_kernel<false, false, true, 0, true>" \
           "r03_gemm:zv_gemm_kernel<128, 128, 2, 2, 1, 0, 2, 2, 64, 0, 0, 0, 3, 1, 0>"; do
   n=${kv%%:*}; rx=${kv#*:}
-  python3 tools/pmc_traffic.py "$F" "$W" "$rx" profiles/${n}_traffic.json >> $O/pmc_traffic.log 2>&1
+  python3 tools/pmc_traffic.py "$F" "$W" "$rx" $O/${n}_traffic.json >> $O/pmc_traffic.log 2>&1
 done
 cat $O/pmc_traffic.log | cut -c1-200
 step bench

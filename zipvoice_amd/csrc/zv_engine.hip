@@ -220,7 +220,9 @@ struct zv_engine {
   // rows; 2 (default): FF3 also carries the layer's BiasNorm + bypass in its epilogue.  C2 bench
   // 445 -> 431 ms per step with the pipelined depthwise conv (profiles/r03_ffn_ab.txt)
   int ffn_fused = 2;
-  long ffn_min_rows = 0;
+  // below ~10k rows (the 4x-downsampled stack's per-stream launches, <= 51 one-per-CU blocks)
+  // the unfused pair fills the chip better: 435 -> 426-432 ms (profiles/r03_ffn_policy_ab.txt)
+  long ffn_min_rows = 10000;
   bool ff1_src = true;             // ZV_FF1_SRC: FF1's residual read as src + temb (row vector) instead
                                    // of a working stream BiasNorm / the stack entry wrote in fp32
   bool sa_copy = true;             // ZV_SA_COPY: the copy-only SelfAttention out-projection on the
@@ -281,7 +283,7 @@ struct zv_engine {
     n96_mode = envi("ZV_N96", 2);
     ff1_src = envi("ZV_FF1_SRC", 1) != 0;
     ffn_fused = envi("ZV_FFN", 2);
-    ffn_min_rows = envi("ZV_FFN_MIN_ROWS", 0);
+    ffn_min_rows = envi("ZV_FFN_MIN_ROWS", 10000);
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
