@@ -35,4 +35,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/rp -o run -- pyt
 step trace
 bash tools/gpu/r03_trace.sh final_trace - > $O/trace.log 2>&1 || { tail -5 $O/trace.log; exit 1; }
 tail -20 $O/trace.log
+step mx8_align
+timeout -k 10 60 tools/probe/mx8_align > $O/mx8_align.txt 2>&1 || { tail -5 $O/mx8_align.txt; exit 1; }
 step done

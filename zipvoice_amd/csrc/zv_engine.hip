@@ -216,13 +216,17 @@ struct zv_engine {
                                    // out-projections 50.0 -> 28.7 ms per step, profiles/r02_fp8_ws_ab.txt)
   int n96_mode = 2;                // ZV_N96: the attention-score projection's tiles (see linear16)
   // ZV_FFN: the decoder FeedForward modules as one fused kernel each (zv_ffn.inc: in_proj ->
-  // SwooshL -> out_proj -> residual without the hidden tensor in HBM) for at least ffn_min_rows
-  // rows; 2 (default): FF3 also carries the layer's BiasNorm + bypass in its epilogue.  C2 bench
-  // 445 -> 431 ms per step with the pipelined depthwise conv (profiles/r03_ffn_ab.txt)
+  // SwooshL -> out_proj -> residual without the hidden tensor in HBM) in stacks of at least
+  // ffn_min_frames frames; 2 (default): FF3 also carries the layer's BiasNorm + bypass in its
+  // epilogue.  C2 bench 445 -> 431 ms per step with the pipelined depthwise conv
+  // (profiles/r03_ffn_ab.txt)
   int ffn_fused = 2;
-  // below ~10k rows (the 4x-downsampled stack's per-stream launches, <= 51 one-per-CU blocks)
-  // the unfused pair fills the chip better: 435 -> 426-432 ms (profiles/r03_ffn_policy_ab.txt)
-  long ffn_min_rows = 10000;
+  // ZV_FFN_MIN_FRAMES: the 4x / 8x-downsampled stacks (305 / 153 frames at C2: <= 51 one-per-CU
+  // blocks per decoder stream) run the unfused pair, which fills the chip better there
+  // (profiles/r03_ffn_policy_ab.txt).  The threshold is on the stack's frame count, not on the
+  // launch's rows, so the kernel choice - and the arithmetic - of an utterance does not depend
+  // on the batch it is in or on the stream split (tests/test_gpu_fullsize.py batch rows test)
+  int ffn_min_frames = 500;
   bool ff1_src = true;             // ZV_FF1_SRC: FF1's residual read as src + temb (row vector) instead
                                    // of a working stream BiasNorm / the stack entry wrote in fp32
   bool sa_copy = true;             // ZV_SA_COPY: the copy-only SelfAttention out-projection on the
@@ -283,7 +287,7 @@ struct zv_engine {
     n96_mode = envi("ZV_N96", 2);
     ff1_src = envi("ZV_FF1_SRC", 1) != 0;
     ffn_fused = envi("ZV_FFN", 2);
-    ffn_min_rows = envi("ZV_FFN_MIN_ROWS", 10000);
+    ffn_min_frames = envi("ZV_FFN_MIN_FRAMES", 500);
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
@@ -984,7 +988,7 @@ struct zv_engine {
     auto ff = [&](int f, const Out& oe) {
       if constexpr (SPLIT == 1) {
         if (ffn_fused && W.ffn_w1f[f] && !pairm && !(f8 && W.ff_in[f].q8) && oe.C && oe.resid &&
-            !oe.act.l && !oe.residh && M >= ffn_min_rows && cur_a.ld % 8 == 0) {
+            !oe.act.l && !oe.residh && L >= ffn_min_frames && cur_a.ld % 8 == 0) {
           FfnParams q{};
           q.M = (int)M; q.H = W.ff_in[f].N;
           q.X = cur_a.h; q.ldx = cur_a.ld;
@@ -1168,7 +1172,7 @@ struct zv_engine {
     // FF3 + BiasNorm + bypass in the fused FeedForward kernel's norm epilogue (the FF3 output
     // never reaches HBM; zv_ffn.inc)
     const bool ffn_norm = SPLIT == 1 && ffn_fused >= 2 && W.ffn_w1f[2] && !pairm && !f8 && D == FFN_D &&
-                          M >= ffn_min_rows && cur_a.ld == src_a.ld && cur_a.ld % 8 == 0;
+                          L >= ffn_min_frames && cur_a.ld == src_a.ld && cur_a.ld % 8 == 0;
     if (ffn_norm) {
       FfnParams q{};
       q.M = (int)M; q.H = W.ff_in[2].N;
@@ -1302,8 +1306,11 @@ struct zv_engine {
           ZV_LAUNCH_CHECK();
         }
         stack<SPLIT>(Z, S, ws, d, d_a, N, dL, pds, te, s);
-        hipLaunchKernelGGL(zv_upsample_combine_kernel, grid1d(M * D), dim3(256), 0, s, main, d,
-                           S.combiner, main, N, T, dL, D, S.ds);
+        ZV_REQUIRE(D % 4 == 0 && 256 % (D / 4) == 0, "upsample_combine needs 256 % (D/4) == 0");
+        const long rows_per_block = 4L * (256 / (D / 4));
+        hipLaunchKernelGGL(zv_upsample_combine_kernel,
+                           dim3((unsigned)((M + rows_per_block - 1) / rows_per_block)), dim3(256), 0,
+                           s, main, d, S.combiner, main, N, T, dL, D, S.ds);
         ZV_LAUNCH_CHECK();
       }
     }
