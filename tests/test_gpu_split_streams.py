@@ -33,9 +33,12 @@ def test_split_streams_bitwise(monkeypatch, variant, precision, parts):
     x, tc, sc, pm = _inputs(B, T, [1500, 1200, 777], seed=3)
     g_rows = torch.tensor([1.0, 0.0, 2.0]).reshape(B, 1, 1)
     outs = []
-    for flag in ("1", parts):
+    # single stream, split + graph replay, split + plain launches (ZV_GRAPH=2, the default:
+    # split shapes are not replayed from a graph)
+    for flag, graph in (("1", "1"), (parts, "1"), (parts, "2")):
         monkeypatch.setenv("ZV_SPLIT_STREAMS", flag)
         monkeypatch.setenv("ZV_SPLIT_MIN_ROWS", "2048")
+        monkeypatch.setenv("ZV_GRAPH", graph)
         m = build_model(cfg, precision=precision)
         m.load_state_dict(sd)
         m = m.to("cuda:0")
@@ -47,7 +50,8 @@ def test_split_streams_bitwise(monkeypatch, variant, precision, parts):
         r.append(xs.cpu())
         outs.append(r)
         del m
-    for i, (a, b) in enumerate(zip(*outs)):
-        d = (a - b).abs().max().item()
-        print(f"{variant} {precision} output {i}: max |split - single| = {d:.3e}")
-        assert torch.equal(a, b), (i, d)
+    for arm in outs[1:]:
+        for i, (a, b) in enumerate(zip(outs[0], arm)):
+            d = (a - b).abs().max().item()
+            print(f"{variant} {precision} output {i}: max |split - single| = {d:.3e}")
+            assert torch.equal(a, b), (i, d)

@@ -112,6 +112,15 @@ def main():
           f"sum of kernel durations {tot/1e6:.2f} | mean concurrency {tot/busy:.3f}")
     print(f"largest idle gaps (us): {', '.join(f'{g/1e3:.1f}' for g in gaps[:8])}; "
           f"gaps > 10 us per step: {res['gaps_over_10us_per_step']:.1f}")
+    # what borders the largest gaps: the last kernel to end before, the first to start after
+    ends = sorted((e, n) for _, e, n in win)
+    starts = sorted((s, n) for s, _, n in win)
+    for i in sorted(range(len(allv) - 1), key=lambda i: allv[i][1] - allv[i + 1][0])[:4]:
+        g0, g1 = allv[i][1], allv[i + 1][0]
+        before = max((e, n) for e, n in ends if e <= g0)[1]
+        after = min((s, n) for s, n in starts if s >= g1)[1]
+        print(f"  gap {(g1 - g0) / 1e3:9.1f} us at {(g0 - t0) / 1e6:8.2f} ms: after {before[:60]} | "
+              f"before {after[:60]}")
     print(f"{'class':22s} {'disp':>6s} {'sum ms':>8s} {'union ms':>9s} {'alone ms':>9s}")
     for c, v in sorted(byc.items(), key=lambda kv: -sum(e - s for s, e in kv[1])):
         mv = merge(v)

@@ -269,7 +269,7 @@ struct zv_engine {
     const char* e = getenv("ZV_ATTN_MATERIALIZE");
     materialize_attn = e && e[0] == '1';
     const char* gr = getenv("ZV_GRAPH");
-    graphs_enabled = !(gr && gr[0] == '0');
+    graph_mode = gr ? atoi(gr) : 2;
     const char* o1 = getenv("ZV_GEMM_OCC_PLAIN");
     const char* o2 = getenv("ZV_GEMM_OCC_RESID");
     const char* o3 = getenv("ZV_GEMM_OCC_FUSED");
@@ -343,7 +343,13 @@ struct zv_engine {
   hipStream_t gstream = nullptr;
   hipEvent_t gev_in = nullptr, gev_out = nullptr;
   DBuf gx, gtc, gsc, gpad, ggrows;
-  bool graphs_enabled = true;
+  // ZV_GRAPH: 0 plain launches, 1 always replay the captured Euler loop, 2 (default) replay it
+  // unless the decoder splits its rows over streams.  A replayed multi-stream graph ran 10 ms
+  // per C2 step slower than the same launches made directly on the three engine streams
+  // (419.8 vs 410.0 ms, profiles/r03_graph_ab.txt; the runtime's own graph queues add the
+  // cross-branch waits), while single-stream shapes (one sentence) are launch-bound and
+  // need the graph
+  int graph_mode = 2;
   bool io_split = false;           // set per decoder call: ZV_MIXED's split in/out projections
                                    // and attention-score projections
 
@@ -1455,7 +1461,13 @@ struct zv_engine {
                     int num_step, float g, const float* grows, bool cfg_rows, float t0, float t1,
                     float shift, hipStream_t s) {
     const std::vector<float> ts = time_steps(t0, t1, num_step, shift);
-    if (!graphs_enabled || g_zv_prof.on) {
+    bool graph = graph_mode != 0 && !g_zv_prof.on;
+    if (graph && graph_mode == 2) {   // the split test of decoder(), on the CFG-doubled rows
+      const bool cfg_on = !distill() && (grows ? cfg_rows : g != 0.0f);
+      const long N = (cfg_on ? 2L : 1L) * B;
+      graph = !(split_streams >= 2 && N >= 2 && N * T >= split_min_rows);
+    }
+    if (!graph) {
       euler_loop(x, tc, sc, pad, B, T, ts, g, grows, cfg_rows, s);
       return;
     }

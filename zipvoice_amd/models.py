@@ -215,19 +215,27 @@ class ZipVoice:
         elif tuple(x0.shape) != (batch_size, num_frames, F):
             raise ValueError(f"x0 must have shape {(batch_size, num_frames, F)}, got "
                              f"{tuple(x0.shape)}")
+        # the output shapes are known before sampling: reading them here (the text path has
+        # already synchronised for num_frames) keeps the host from waiting on the Euler loop,
+        # so the prompt split and the vocoder are queued behind it without an idle gap
+        x1_wo_prompt_lens = (~padding_mask).sum(-1) - prompt_features_lens
+        Tg, Tp = (int(v) for v in torch.stack([x1_wo_prompt_lens.max(),
+                                                prompt_features_lens.max()]).tolist())
         x1 = self.solver.sample(x=x0, text_condition=text_condition,
                                 speech_condition=speech_condition, padding_mask=padding_mask,
                                 num_step=num_step, guidance_scale=guidance_scale, t_shift=t_shift)
-        x1_wo_prompt_lens = (~padding_mask).sum(-1) - prompt_features_lens
-        return split_prompt(x1, prompt_features_lens, x1_wo_prompt_lens) + (prompt_features_lens,)
+        return split_prompt(x1, prompt_features_lens, x1_wo_prompt_lens, Tg, Tp) + (
+            prompt_features_lens,)
 
 
-def split_prompt(x1: torch.Tensor, prompt_lens: torch.Tensor, gen_lens: torch.Tensor):
-    """zipvoice.py:469-486 without the per-item python slicing loop: one gather."""
+def split_prompt(x1: torch.Tensor, prompt_lens: torch.Tensor, gen_lens: torch.Tensor,
+                 Tg: Optional[int] = None, Tp: Optional[int] = None):
+    """zipvoice.py:469-486 without the per-item python slicing loop: one gather.  Tg / Tp
+    (the longest generated / prompt part) are read from the lengths when not given."""
     B, T, F = x1.shape
     dev = x1.device
-    Tg = int(gen_lens.max())
-    Tp = int(prompt_lens.max())
+    Tg = int(gen_lens.max()) if Tg is None else Tg
+    Tp = int(prompt_lens.max()) if Tp is None else Tp
     ar_g = torch.arange(Tg, device=dev)[None]
     idx = (prompt_lens[:, None] + ar_g).clamp(max=T - 1)
     gen = torch.gather(x1, 1, idx[..., None].expand(B, Tg, F))
