@@ -9,8 +9,8 @@ the fp32 oracle (reference zipformer.py:1433-1439, :610-618; scaling.py:330-355)
 16-bit model those orders flip roundings, so the arms differ by about one mode error from each
 other (the kernel itself matches the unfused pair to 2e-7: tools/lab/ffn_lab,
 profiles/r03_ffn_lab.txt).  The pipelined depthwise conv keeps the register-window kernel's FMA
-order per output: bitwise equal velocities.  ZV_FFN_MIN_FRAMES=0 puts every stack on the fused
-kernel (by default stacks under 500 frames keep the unfused pair)."""
+order per output: bitwise equal velocities.  ZV_FFN_MIN_ROWS=0 puts every launch on the fused
+kernel (by default launches under 10000 rows keep the unfused pair)."""
 import numpy as np
 import pytest
 
@@ -48,7 +48,7 @@ def test_fused_ffn_vs_unfused_and_oracle(monkeypatch, precision):
     from oracle.zipvoice_np import ZipVoiceOracle
     outs = {}
     for ffn in ("0", "1", "2"):
-        outs[ffn], inp = _run(monkeypatch, {"ZV_FFN": ffn, "ZV_FFN_MIN_FRAMES": "0"}, precision)
+        outs[ffn], inp = _run(monkeypatch, {"ZV_FFN": ffn, "ZV_FFN_MIN_ROWS": "0"}, precision)
     cfg, sd, x, tc, sc, pm, t = inp
     ref = ZipVoiceOracle(cfg, sd).velocity(np.float32(t), x, tc, sc, pm, 1.0)
     valid = ~pm
@@ -72,7 +72,7 @@ def test_fused_ffn_long_ragged(monkeypatch):
     """A length whose row counts are not multiples of the 128-row block at any stack's rate
     (2 CFG rows x 1001 frames; every downsampling factor's FF widths), fp16 parity mode."""
     from oracle.zipvoice_np import ZipVoiceOracle
-    o, inp = _run(monkeypatch, {"ZV_FFN": "2", "ZV_FFN_MIN_FRAMES": "0"}, "fp16", B=1, T=1001, lens=(1001,), t=0.6)
+    o, inp = _run(monkeypatch, {"ZV_FFN": "2", "ZV_FFN_MIN_ROWS": "0"}, "fp16", B=1, T=1001, lens=(1001,), t=0.6)
     cfg, sd, x, tc, sc, pm, t = inp
     ref = ZipVoiceOracle(cfg, sd).velocity(np.float32(t), x, tc, sc, pm, 1.0)
     e = np.abs(o - ref)[~pm]

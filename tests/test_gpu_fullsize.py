@@ -94,13 +94,22 @@ def test_velocity_full_size_vs_oracle(name, precision):
     check(v, _refs[name], precision, f"{name} velocity B={B} T={T} t={t} g={g}")
 
 
-def test_c2_batch_rows_equal_single_utterance():
+def test_c2_batch_rows_equal_single_utterance(monkeypatch):
     """The C2 bench shape (32 utterances = 64 CFG rows, T = 1219, bf16): each row of the
     batched velocity equals the single-utterance run (rows are independent: no
-    cross-row arithmetic anywhere on the path), and row 0 matches the oracle."""
+    cross-row arithmetic anywhere on the path), and row 0 matches the oracle.  The
+    FeedForward kernel is chosen by launch rows (fused from ZV_FFN_MIN_ROWS = 10000 rows
+    by default), so a batch-invariant engine pins the choice: ZV_FFN_MIN_ROWS=0."""
     B, T = 32, 1219
     x, tc, sc, pm = inputs(B, T, 100, [T] * B, seed=21)
-    m = model("zipvoice", "bf16")
+    from zipvoice_amd.config import default_config
+    from zipvoice_amd.models import build_model
+    from zipvoice_amd.weights import synthetic_state_dict
+    monkeypatch.setenv("ZV_FFN_MIN_ROWS", "0")
+    cfg = default_config("zipvoice")
+    m = build_model(cfg, precision="bf16")
+    m.load_state_dict(synthetic_state_dict(cfg, 0))
+    m = m.to("cuda:0")
     vb = m.engine.velocity(0.3, 1.0, cuda(x), cuda(tc), cuda(sc), None).cpu()
     for b in (0, 13, 31):
         v1 = m.engine.velocity(0.3, 1.0, cuda(x[b:b + 1]), cuda(tc[b:b + 1]), cuda(sc[b:b + 1]),

@@ -39,6 +39,7 @@ def test_split_streams_bitwise(monkeypatch, variant, precision, parts):
         monkeypatch.setenv("ZV_SPLIT_STREAMS", flag)
         monkeypatch.setenv("ZV_SPLIT_MIN_ROWS", "2048")
         monkeypatch.setenv("ZV_GRAPH", graph)
+        monkeypatch.setenv("ZV_FFN_MIN_ROWS", "0")    # one FeedForward kernel at every block size
         m = build_model(cfg, precision=precision)
         m.load_state_dict(sd)
         m = m.to("cuda:0")

@@ -12,6 +12,7 @@
 
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -168,6 +169,24 @@ struct Workspace {
   }
 };
 
+// Engine streams come from a per-device process-wide pool, created once and never destroyed.
+// Streams are multiplexed onto the process's few hardware queues (GPU_MAX_HW_QUEUES, 4);
+// streams created after others were destroyed were mapped so that the decoder's row blocks
+// shared queues: a second engine in one process ran C5 at 341 ms per step against 216 ms
+// for the first (profiles/r03_stream_pool_ab.txt).  Reusing the first engine's streams
+// keeps every engine on the mapping of the first.
+static hipStream_t pooled_stream(int slot) {
+  constexpr int DEVS = 16, SLOTS = 8;
+  static hipStream_t pool[DEVS][SLOTS] = {};
+  static std::mutex mu;
+  int dev = 0;
+  ZV_CHECK(hipGetDevice(&dev));
+  ZV_REQUIRE(dev >= 0 && dev < DEVS && slot >= 0 && slot < SLOTS, "stream pool index");
+  std::lock_guard<std::mutex> lock(mu);
+  if (!pool[dev][slot]) ZV_CHECK(hipStreamCreateWithFlags(&pool[dev][slot], hipStreamNonBlocking));
+  return pool[dev][slot];
+}
+
 inline dim3 grid1d(long n, int block = 256) {
   long g = (n + block - 1) / block;
   if (g > 65536) g = 65536;
@@ -216,17 +235,20 @@ struct zv_engine {
                                    // out-projections 50.0 -> 28.7 ms per step, profiles/r02_fp8_ws_ab.txt)
   int n96_mode = 2;                // ZV_N96: the attention-score projection's tiles (see linear16)
   // ZV_FFN: the decoder FeedForward modules as one fused kernel each (zv_ffn.inc: in_proj ->
-  // SwooshL -> out_proj -> residual without the hidden tensor in HBM) in stacks of at least
-  // ffn_min_frames frames; 2 (default): FF3 also carries the layer's BiasNorm + bypass in its
+  // SwooshL -> out_proj -> residual without the hidden tensor in HBM) for launches of at
+  // least ffn_min_rows rows; 2 (default): FF3 also carries the layer's BiasNorm + bypass in its
   // epilogue.  C2 bench 445 -> 431 ms per step with the pipelined depthwise conv
   // (profiles/r03_ffn_ab.txt)
   int ffn_fused = 2;
-  // ZV_FFN_MIN_FRAMES: the 4x / 8x-downsampled stacks (305 / 153 frames at C2: <= 51 one-per-CU
-  // blocks per decoder stream) run the unfused pair, which fills the chip better there
-  // (profiles/r03_ffn_policy_ab.txt).  The threshold is on the stack's frame count, not on the
-  // launch's rows, so the kernel choice - and the arithmetic - of an utterance does not depend
-  // on the batch it is in or on the stream split (tests/test_gpu_fullsize.py batch rows test)
-  int ffn_min_frames = 500;
+  // ZV_FFN_MIN_ROWS: launches under this many rows run the unfused pair, which fills the chip
+  // better there (a fused block owns a CU and takes 128 rows: 10k rows = 78 blocks for 256
+  // CUs).  C2 435 -> 426-432 ms (profiles/r03_ffn_policy_ab.txt); C3 (16 utterances, no
+  // CFG: ~6.5k rows per decoder stream) 88.4 -> 74.6 ms and C5 246 -> 220 ms with the pair
+  // (profiles/r03_ffn_configs_ab.txt).  The choice follows the launch's rows, so an
+  // utterance's rounding can depend on its batch (as any shape-dependent kernel choice);
+  // ZV_FFN_MIN_ROWS=0 pins the fused kernel for a batch-invariant engine
+  // (tests/test_gpu_fullsize.py batch rows test)
+  long ffn_min_rows = 10000;
   bool ff1_src = true;             // ZV_FF1_SRC: FF1's residual read as src + temb (row vector) instead
                                    // of a working stream BiasNorm / the stack entry wrote in fp32
   bool sa_copy = true;             // ZV_SA_COPY: the copy-only SelfAttention out-projection on the
@@ -287,7 +309,7 @@ struct zv_engine {
     n96_mode = envi("ZV_N96", 2);
     ff1_src = envi("ZV_FF1_SRC", 1) != 0;
     ffn_fused = envi("ZV_FFN", 2);
-    ffn_min_frames = envi("ZV_FFN_MIN_FRAMES", 500);
+    ffn_min_rows = envi("ZV_FFN_MIN_ROWS", 10000);
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
@@ -369,11 +391,12 @@ struct zv_engine {
 
   ~zv_engine() {
     drop_graphs();
-    if (gstream) (void)hipStreamDestroy(gstream);
+    // pooled streams outlive the engine: drain what this engine queued on them
+    if (gstream) (void)hipStreamSynchronize(gstream);
     if (gev_in) (void)hipEventDestroy(gev_in);
     if (gev_out) (void)hipEventDestroy(gev_out);
     for (int i = 0; i < MAX_SPLIT - 1; ++i) {
-      if (split_stream[i]) (void)hipStreamDestroy(split_stream[i]);
+      if (split_stream[i]) (void)hipStreamSynchronize(split_stream[i]);
       if (split_join[i]) (void)hipEventDestroy(split_join[i]);
     }
     if (split_fork) (void)hipEventDestroy(split_fork);
@@ -994,7 +1017,7 @@ struct zv_engine {
     auto ff = [&](int f, const Out& oe) {
       if constexpr (SPLIT == 1) {
         if (ffn_fused && W.ffn_w1f[f] && !pairm && !(f8 && W.ff_in[f].q8) && oe.C && oe.resid &&
-            !oe.act.l && !oe.residh && L >= ffn_min_frames && cur_a.ld % 8 == 0) {
+            !oe.act.l && !oe.residh && M >= ffn_min_rows && cur_a.ld % 8 == 0) {
           FfnParams q{};
           q.M = (int)M; q.H = W.ff_in[f].N;
           q.X = cur_a.h; q.ldx = cur_a.ld;
@@ -1178,7 +1201,7 @@ struct zv_engine {
     // FF3 + BiasNorm + bypass in the fused FeedForward kernel's norm epilogue (the FF3 output
     // never reaches HBM; zv_ffn.inc)
     const bool ffn_norm = SPLIT == 1 && ffn_fused >= 2 && W.ffn_w1f[2] && !pairm && !f8 && D == FFN_D &&
-                          L >= ffn_min_frames && cur_a.ld == src_a.ld && cur_a.ld % 8 == 0;
+                          M >= ffn_min_rows && cur_a.ld == src_a.ld && cur_a.ld % 8 == 0;
     if (ffn_norm) {
       FfnParams q{};
       q.M = (int)M; q.H = W.ff_in[2].N;
@@ -1366,7 +1389,7 @@ struct zv_engine {
     if (!split_fork) {
       ZV_CHECK(hipEventCreateWithFlags(&split_fork, hipEventDisableTiming));
       for (int i = 0; i < MAX_SPLIT - 1; ++i) {
-        ZV_CHECK(hipStreamCreateWithFlags(&split_stream[i], hipStreamNonBlocking));
+        split_stream[i] = pooled_stream(i);
         ZV_CHECK(hipEventCreateWithFlags(&split_join[i], hipEventDisableTiming));
       }
     }
@@ -1489,7 +1512,7 @@ struct zv_engine {
       return;
     }
     if (!gstream) {
-      ZV_CHECK(hipStreamCreateWithFlags(&gstream, hipStreamNonBlocking));
+      gstream = pooled_stream(MAX_SPLIT - 1);
       ZV_CHECK(hipEventCreateWithFlags(&gev_in, hipEventDisableTiming));
       ZV_CHECK(hipEventCreateWithFlags(&gev_out, hipEventDisableTiming));
     }
