@@ -13,7 +13,7 @@ for r in 1; do
   done
 done
 cat $O/lab.txt
-ZV_LIB_PATH=$T1 timeout -k 10 600 python -u -m pytest tests/test_gpu_ffn.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -q \
+ZV_LIB_PATH=$T1 ZV_LIB_F16_PATH=zipvoice_amd/libzipvoice_hip_f16_tail1.so timeout -k 10 600 python -u -m pytest tests/test_gpu_ffn.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -q \
   --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 bash tools/gpu/ab_env.sh tail/ab ${1:-2} "-" "ZV_LIB_PATH=$T1"

@@ -111,11 +111,12 @@ _lib = None            # the main (bf16-operand) library
 def load_library(path: Optional[str] = None, operand: str = "bf16"):
     """dlopen the engine (fails loudly when it has not been built).  operand "f16" loads the
     fp16-operand build.  ZV_LIB_PATH selects an alternative build of the main library (A/B
-    measurements).  Both are loaded RTLD_LOCAL (and linked -Bsymbolic): the two libraries
+    measurements), ZV_LIB_F16_PATH one of the fp16-operand library.  Both are loaded RTLD_LOCAL (and linked -Bsymbolic): the two libraries
     export the same entry points and each binds its own."""
     global _lib
     if path is None:
-        path = LIB_F16_PATH if operand == "f16" else (os.environ.get("ZV_LIB_PATH") or LIB_PATH)
+        path = ((os.environ.get("ZV_LIB_F16_PATH") or LIB_F16_PATH) if operand == "f16"
+                else (os.environ.get("ZV_LIB_PATH") or LIB_PATH))
     if path in _libs:
         return _libs[path]
     if not os.path.exists(path):
