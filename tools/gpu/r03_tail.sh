@@ -1,7 +1,11 @@
 #!/bin/bash
 # Fused FF tail (FFN_TAIL): lab old vs new (same results expected bit for bit), the FF GPU tests
 # + parity / fullsize on the FFN_TAIL=1 library (ZV_LIB_PATH), then the C2 bench A/B (the default
-# library vs the FFN_TAIL=1 one), interleaved.
+# library vs the FFN_TAIL=1 one), interleaved.  Build first, on the CPU:
+#   python zipvoice_amd/csrc/build.py --out zipvoice_amd/libzipvoice_hip_tail1.so -DFFN_TAIL=1
+#   python zipvoice_amd/csrc/build.py --out zipvoice_amd/libzipvoice_hip_f16_tail1.so -DFFN_TAIL=1 -DZV_OPERAND_F16
+#   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I zipvoice_amd/csrc tools/lab/ffn_lab.hip -DFFN_TAIL=1 -o tools/lab/ffn_lab
+#   (and -DFFN_TAIL=0 -o tools/lab/ffn_lab_old)
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 O=gpurun_out/tail; mkdir -p $O
