@@ -56,3 +56,41 @@ def test_split_streams_bitwise(monkeypatch, variant, precision, parts):
             d = (a - b).abs().max().item()
             print(f"{variant} {precision} output {i}: max |split - single| = {d:.3e}")
             assert torch.equal(a, b), (i, d)
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_ffn_persistent_and_joined_bitwise(monkeypatch, precision):
+    """The fused FeedForward's persistent line schedule (ZV_FFN_PERSIST, zv_ffn.inc: row blocks cut
+    into P / C items whose out^T tiles are handed over through memory) and the joined launch over
+    the split decoder's row blocks (ZV_FFN_JOIN: one launch, one row range per stream) against one
+    row block per block on one stream, with the default thresholds: bitwise equal velocities.
+    16 utterances = 32 CFG rows x 1219 frames: 39008 rows (305 row blocks) at the full-rate stacks,
+    19504 at the half-rate ones -- lines cut row blocks at every stack that runs fused."""
+    from zipvoice_amd.config import default_config
+    from zipvoice_amd.models import build_model
+    from zipvoice_amd.weights import synthetic_state_dict
+    cfg = default_config("zipvoice")
+    sd = synthetic_state_dict(cfg, 0)
+    B, T = 16, 1219
+    x, tc, sc, pm = _inputs(B, T, [1219 - 37 * i for i in range(B)], seed=5)
+    outs = []
+    for env in ({"ZV_SPLIT_STREAMS": "1", "ZV_FFN_PERSIST": "0"},
+                {"ZV_SPLIT_STREAMS": "1", "ZV_FFN_PERSIST": "1"},
+                {"ZV_SPLIT_STREAMS": "3", "ZV_FFN_JOIN": "1", "ZV_FFN_PERSIST": "1"},
+                {"ZV_SPLIT_STREAMS": "3", "ZV_FFN_JOIN": "0", "ZV_FFN_PERSIST": "1"}):
+        for k in ("ZV_SPLIT_STREAMS", "ZV_FFN_JOIN", "ZV_FFN_PERSIST", "ZV_FFN_MIN_ROWS", "ZV_GRAPH"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        m = build_model(cfg, precision=precision)
+        m.load_state_dict(sd)
+        m = m.to("cuda:0")
+        outs.append([m.engine.velocity(0.3, 1.0, x, tc, sc, pm).cpu(),
+                     m.engine.velocity(0.8, 1.0, x, tc, sc, pm).cpu()])
+        del m
+    for j, arm in enumerate(outs[1:], 1):
+        for i, (a, b) in enumerate(zip(outs[0], arm)):
+            d = (a - b).abs().max().item()
+            print(f"{precision} arm {j} output {i}: max |arm - classic one-stream| = {d:.3e}")
+            assert torch.isfinite(b).all()
+            assert torch.equal(a, b), (j, i, d)

@@ -14,8 +14,12 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <exception>
+#include <functional>
 #include <tuple>
 #include <vector>
+
+#include <ucontext.h>
 
 #include "zv_common.h"
 #include "zv_gemm.inc"
@@ -157,10 +161,13 @@ struct Workspace {
   ActBuf cur8;   // fp8 mode: the working stream's MX-fp8 copy
   ActBuf dwo;    // bf16 mode: [depthwise-conv output | SelfAttention output] (the K-concatenated
                  // out-projection's operand)
+  // the fused FeedForward's persistent schedule (zv_ffn.inc): one 256 KiB tile slot per CU, one
+  // flag word per CU (zero between launches) and the spin-timeout counter
+  DBuf ffn_part, ffn_flag;
   size_t bytes() const {
     size_t s = 0;
     for (const DBuf* b : {&main, &dsrc, &cur, &temb0, &temb1, &tstack, &tvec, &gvec, &posP, &mask2,
-                          &maskds, &vout, &stats})
+                          &maskds, &vout, &stats, &ffn_part, &ffn_flag})
       s += b->bytes;
     for (const ActBuf* b : {&xin, &main_a, &dsrc_a, &cur_a, &qkp, &W, &hidden, &na_y, &na_xt, &na_o,
                             &sa_vt, &sa_o, &glu, &dw, &emb, &cur8, &dwo})
@@ -169,22 +176,41 @@ struct Workspace {
   }
 };
 
-// Engine streams come from a per-device process-wide pool, created once and never destroyed.
-// Streams are multiplexed onto the process's few hardware queues (GPU_MAX_HW_QUEUES, 4);
-// streams created after others were destroyed were mapped so that the decoder's row blocks
-// shared queues: a second engine in one process ran C5 at 341 ms per step against 216 ms
-// for the first (profiles/r03_stream_pool_ab.txt).  Reusing the first engine's streams
-// keeps every engine on the mapping of the first.
-static hipStream_t pooled_stream(int slot) {
-  constexpr int DEVS = 16, SLOTS = 8;
-  static hipStream_t pool[DEVS][SLOTS] = {};
-  static std::mutex mu;
+// Engine streams come from a per-device process-wide pool of stream sets: an engine takes a set
+// for its lifetime (its decoder row-block streams and its graph stream) and returns it when it is
+// destroyed; a later engine reuses a returned set.  Streams are multiplexed onto the process's few
+// hardware queues (GPU_MAX_HW_QUEUES, 4); streams created after others were destroyed were mapped
+// so that the decoder's row blocks shared queues: a second engine in one process ran C5 at 341 ms
+// per step against 216 ms for the first (profiles/r03_stream_pool_ab.txt).  Reusing sets keeps
+// every engine on the mapping of the first, and no two live engines share a stream (one engine
+// capturing its Euler-loop graph while another launches on the same stream would corrupt both).
+constexpr int ZV_STREAM_SET = 4;
+struct StreamSet { hipStream_t s[ZV_STREAM_SET] = {}; int dev = -1; };
+static std::mutex g_stream_pool_mu;
+static std::vector<StreamSet>& stream_pool_free() { static std::vector<StreamSet> v; return v; }
+static StreamSet acquire_stream_set() {
   int dev = 0;
   ZV_CHECK(hipGetDevice(&dev));
-  ZV_REQUIRE(dev >= 0 && dev < DEVS && slot >= 0 && slot < SLOTS, "stream pool index");
-  std::lock_guard<std::mutex> lock(mu);
-  if (!pool[dev][slot]) ZV_CHECK(hipStreamCreateWithFlags(&pool[dev][slot], hipStreamNonBlocking));
-  return pool[dev][slot];
+  {
+    std::lock_guard<std::mutex> lock(g_stream_pool_mu);
+    auto& fr = stream_pool_free();
+    for (size_t i = 0; i < fr.size(); ++i)
+      if (fr[i].dev == dev) {
+        StreamSet set = fr[i];
+        fr.erase(fr.begin() + i);
+        return set;
+      }
+  }
+  StreamSet set;
+  set.dev = dev;
+  for (auto& st : set.s) ZV_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  return set;
+}
+static void release_stream_set(const StreamSet& set) {
+  if (set.dev < 0) return;
+  for (hipStream_t st : set.s) (void)hipStreamSynchronize(st);
+  std::lock_guard<std::mutex> lock(g_stream_pool_mu);
+  stream_pool_free().push_back(set);
 }
 
 inline dim3 grid1d(long n, int block = 256) {
@@ -310,6 +336,9 @@ struct zv_engine {
     ff1_src = envi("ZV_FF1_SRC", 1) != 0;
     ffn_fused = envi("ZV_FFN", 2);
     ffn_min_rows = envi("ZV_FFN_MIN_ROWS", 10000);
+    ffn_join = envi("ZV_FFN_JOIN", 0);
+    ffn_split_blocks = envi("ZV_FFN_SPLIT_BLOCKS", 0);
+    ffn_persist = envi("ZV_FFN_PERSIST", 1);
     skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
     defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
     pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
@@ -375,6 +404,153 @@ struct zv_engine {
   bool io_split = false;           // set per decoder call: ZV_MIXED's split in/out projections
                                    // and attention-score projections
 
+  // ---------------------------------------------------------------- joined FeedForward
+  // ZV_FFN_PERSIST (default 1): fused FeedForward launches on the persistent line schedule
+  // (zv_ffn.inc; results equal to one row block per block bit for bit).  ZV_FFN_JOIN (default 1):
+  // with the decoder's rows split over streams, the row blocks' FeedForward modules run as ONE
+  // launch over all rows: the line schedule needs the whole batch (C2 per stream: 204 row blocks
+  // for 256 CUs -- one round at best -- against 610 as one launch, 2.4 rounds of work in 2.42).
+  // The row blocks' host code runs as coroutines (ucontext) on the calling thread: each runs until
+  // its next FeedForward (recording an event on its stream), then the engine makes stream 0 wait
+  // for the others, launches once over the row ranges (FfnParams::seg), records an event the
+  // others wait for, and resumes them.  Every kernel stays on its row block's stream; only the
+  // FeedForward joins.
+  struct FfnCo {
+    struct Part {
+      ucontext_t ctx;
+      std::unique_ptr<char[]> stack;
+      std::function<void()> fn;
+      bool done = false, at_site = false;
+      std::exception_ptr err;
+      FfnParams q{};
+      hipStream_t s = nullptr;
+      const char* tag = nullptr;
+      int site = 0;
+    };
+    bool active = false, abort = false;
+    int n = 0, cur = 0;
+    Part part[MAX_SPLIT];
+    ucontext_t sched;
+    hipEvent_t ev_ready[MAX_SPLIT] = {}, ev_done = nullptr;
+  } co;
+  static constexpr size_t CO_STACK = 8u << 20;
+  int ffn_join = 0, ffn_persist = 1, ffn_split_blocks = 0;
+  int dec_parts = 0;               // row blocks of the split decoder while it runs (0: not split)
+  long dec_rows_N = 0;             // the whole batch's rows while a split decoder runs (0: not split):
+                                   // the fused / unfused choice follows the batch, not the row block
+
+  static void co_entry(int lo, int hi) {
+    zv_engine* e = reinterpret_cast<zv_engine*>(((uintptr_t)(unsigned)hi << 32) | (uintptr_t)(unsigned)lo);
+    FfnCo::Part& pt = e->co.part[e->co.cur];
+    try {
+      pt.fn();
+    } catch (...) {
+      pt.err = std::current_exception();
+    }
+    pt.done = true;   // returns into co.sched (uc_link)
+  }
+  void attach_ffn_scratch(FfnParams& q, Workspace& ws) {
+    if (!ffn_persist) return;
+    const int cus = zv_num_cus();
+    q.part = ws.ffn_part.get<float>((size_t)cus * FFN_PART_FLOATS);
+    unsigned* fl = ws.ffn_flag.get<unsigned>((size_t)cus + 64);
+    q.flag = fl;
+    q.err = fl + cus + 32;
+  }
+  // one fused FeedForward launch, or this row block's range of the joined one
+  void ffn_site(FfnParams q, Workspace& ws, hipStream_t s, const char* tag) {
+    if (co.active) {
+      FfnCo::Part& me = co.part[co.cur];
+      me.q = q; me.s = s; me.tag = tag; ++me.site; me.at_site = true;
+      if (co.cur > 0) ZV_CHECK(hipEventRecord(co.ev_ready[co.cur], s));
+      swapcontext(&me.ctx, &co.sched);
+      if (co.abort) throw std::runtime_error("split decoder aborted: another row block failed");
+      return;
+    }
+    attach_ffn_scratch(q, ws);
+    // a row block's launch on the split decoder: its share of the CUs (the blocks' streams run
+    // their FeedForward modules at about the same time; ZV_FFN_SPLIT_BLOCKS overrides)
+    int bmax = 0;
+    if (dec_parts > 1) bmax = ffn_split_blocks > 0 ? ffn_split_blocks : cdiv(zv_num_cus(), dec_parts);
+    launch_ffn(q, s, tag, bmax);
+  }
+  void ffn_join_launch() {
+    FfnCo::Part& p0 = co.part[0];
+    FfnParams q = p0.q;
+    q.nseg = co.n;
+    for (int i = 1; i < co.n; ++i) {
+      const FfnCo::Part& pi = co.part[i];
+      const FfnParams& o = pi.q;
+      ZV_REQUIRE(o.nseg == 1 && pi.site == p0.site && pi.tag == p0.tag && o.H == q.H && o.W1f == q.W1f &&
+                     o.W2f == q.W2f && o.b1 == q.b1 && o.b2 == q.b2 && o.byp == q.byp && o.nb == q.nb &&
+                     o.log_scale == q.log_scale && o.ldx == q.ldx && o.ldc == q.ldc && o.ldch == q.ldch &&
+                     o.rowvec_ld == q.rowvec_ld && o.rows_per_group == q.rows_per_group,
+                 "joined FeedForward: the row blocks reached different FeedForward launches");
+      q.seg[i] = o.seg[0];
+      ZV_CHECK(hipStreamWaitEvent(p0.s, co.ev_ready[i], 0));
+    }
+    attach_ffn_scratch(q, ws_dec);
+    launch_ffn(q, p0.s, p0.tag);
+    ZV_CHECK(hipEventRecord(co.ev_done, p0.s));
+    for (int i = 1; i < co.n; ++i) ZV_CHECK(hipStreamWaitEvent(co.part[i].s, co.ev_done, 0));
+  }
+  // run the row blocks' host code fn[0..n) as coroutines, joining them at every FeedForward
+  void run_joined(std::vector<std::function<void()>>& fns) {
+    co.n = (int)fns.size();
+    co.abort = false;
+    if (!co.ev_done) {
+      ZV_CHECK(hipEventCreateWithFlags(&co.ev_done, hipEventDisableTiming));
+      for (int i = 0; i < MAX_SPLIT; ++i) ZV_CHECK(hipEventCreateWithFlags(&co.ev_ready[i], hipEventDisableTiming));
+    }
+    for (int i = 0; i < co.n; ++i) {
+      FfnCo::Part& pt = co.part[i];
+      pt.fn = std::move(fns[i]);
+      pt.done = pt.at_site = false;
+      pt.err = nullptr;
+      pt.site = 0;
+      if (!pt.stack) pt.stack.reset(new char[CO_STACK]);
+      ZV_REQUIRE(getcontext(&pt.ctx) == 0, "getcontext");
+      pt.ctx.uc_stack.ss_sp = pt.stack.get();
+      pt.ctx.uc_stack.ss_size = CO_STACK;
+      pt.ctx.uc_link = &co.sched;
+      makecontext(&pt.ctx, (void (*)())co_entry, 2, (int)(unsigned)(uintptr_t)this,
+                  (int)(unsigned)((uintptr_t)this >> 32));
+    }
+    std::exception_ptr first;
+    co.active = true;
+    for (;;) {
+      for (int i = 0; i < co.n; ++i) {
+        FfnCo::Part& pt = co.part[i];
+        if (pt.done) continue;
+        co.cur = i;
+        pt.at_site = false;
+        swapcontext(&co.sched, &pt.ctx);
+      }
+      int ndone = 0, nsite = 0;
+      for (int i = 0; i < co.n; ++i) {
+        ndone += co.part[i].done;
+        nsite += co.part[i].at_site;
+        if (co.part[i].err && !first) first = co.part[i].err;
+      }
+      if (ndone == co.n) break;
+      if (first) { co.abort = true; continue; }          // resume the others: they unwind
+      if (nsite != co.n) {
+        first = std::make_exception_ptr(std::runtime_error("joined FeedForward: a row block finished early"));
+        co.abort = true;
+        continue;
+      }
+      try {
+        ffn_join_launch();
+      } catch (...) {
+        first = std::current_exception();
+        co.abort = true;
+      }
+    }
+    co.active = false;
+    for (int i = 0; i < co.n; ++i) co.part[i].fn = nullptr;
+    if (first) std::rethrow_exception(first);
+  }
+
   void drop_graphs() {
     for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
     graphs.clear();
@@ -389,17 +565,25 @@ struct zv_engine {
     graphs.erase(victim);
   }
 
+  StreamSet streams;                // this engine's stream set (acquire_stream_set), taken lazily
+  hipStream_t engine_stream(int slot) {
+    static_assert(MAX_SPLIT <= ZV_STREAM_SET, "stream set holds the split streams and the graph stream");
+    if (streams.dev < 0) streams = acquire_stream_set();
+    return streams.s[slot];
+  }
+
   ~zv_engine() {
     drop_graphs();
-    // pooled streams outlive the engine: drain what this engine queued on them
-    if (gstream) (void)hipStreamSynchronize(gstream);
+    // the stream set outlives the engine: drain what this engine queued on it, then return it
+    release_stream_set(streams);
     if (gev_in) (void)hipEventDestroy(gev_in);
     if (gev_out) (void)hipEventDestroy(gev_out);
-    for (int i = 0; i < MAX_SPLIT - 1; ++i) {
-      if (split_stream[i]) (void)hipStreamSynchronize(split_stream[i]);
+    for (int i = 0; i < MAX_SPLIT - 1; ++i)
       if (split_join[i]) (void)hipEventDestroy(split_join[i]);
-    }
     if (split_fork) (void)hipEventDestroy(split_fork);
+    for (int i = 0; i < MAX_SPLIT; ++i)
+      if (co.ev_ready[i]) (void)hipEventDestroy(co.ev_ready[i]);
+    if (co.ev_done) (void)hipEventDestroy(co.ev_done);
     for (void* p : allocs) (void)hipFree(p);
   }
 
@@ -957,6 +1141,9 @@ struct zv_engine {
              const float* temb, bool has_next, hipStream_t s, bool fresh8 = false) {
     const bool split = SPLIT == 3;
     const long M = (long)B * L;
+    // the batch's rows: the fused / unfused FeedForward choice must not depend on how the decoder
+    // split its rows over streams (every row block makes the same choice; bitwise equal to one stream)
+    const long Mtot = dec_rows_N > 0 ? dec_rows_N * (long)L : M;
     const int D = Z.dim, H = Z.heads;
     const long Lpad = round_up(L, 64);
     const char* tag_att = split ? "gemm_attn_fp32" : "gemm_attn_bf16";
@@ -1017,15 +1204,16 @@ struct zv_engine {
     auto ff = [&](int f, const Out& oe) {
       if constexpr (SPLIT == 1) {
         if (ffn_fused && W.ffn_w1f[f] && !pairm && !(f8 && W.ff_in[f].q8) && oe.C && oe.resid &&
-            !oe.act.l && !oe.residh && M >= ffn_min_rows && cur_a.ld % 8 == 0) {
+            !oe.act.l && !oe.residh && Mtot >= ffn_min_rows && cur_a.ld % 8 == 0) {
           FfnParams q{};
-          q.M = (int)M; q.H = W.ff_in[f].N;
-          q.X = cur_a.h; q.ldx = cur_a.ld;
+          q.H = W.ff_in[f].N; q.nseg = 1;
+          FfnSeg& g = q.seg[0];
+          g.M = (int)M; g.X = cur_a.h; q.ldx = cur_a.ld;
           q.W1f = W.ffn_w1f[f]; q.b1 = W.ff_in[f].b; q.W2f = W.ffn_w2f[f]; q.b2 = W.ff_out[f].b;
-          q.resid = oe.resid; q.C = oe.C; q.ldc = oe.ldc; q.Ch = oe.act.h; q.ldch = oe.act.ld;
-          q.rowvec = oe.rowvec; q.rowvec_ld = oe.rowvec_ld; q.rows_per_group = oe.rows_per_group;
-          q.orig = oe.orig; q.byp = oe.byp;
-          launch_ffn(q, s, "ffn_bf16");
+          g.resid = oe.resid; g.C = oe.C; q.ldc = oe.ldc; g.Ch = oe.act.h; q.ldch = oe.act.ld;
+          g.rowvec = oe.rowvec; q.rowvec_ld = oe.rowvec_ld; q.rows_per_group = oe.rows_per_group;
+          g.orig = oe.orig; q.byp = oe.byp;
+          ffn_site(q, ws, s, "ffn_bf16");
           return;
         }
       }
@@ -1201,19 +1389,20 @@ struct zv_engine {
     // FF3 + BiasNorm + bypass in the fused FeedForward kernel's norm epilogue (the FF3 output
     // never reaches HBM; zv_ffn.inc)
     const bool ffn_norm = SPLIT == 1 && ffn_fused >= 2 && W.ffn_w1f[2] && !pairm && !f8 && D == FFN_D &&
-                          M >= ffn_min_rows && cur_a.ld == src_a.ld && cur_a.ld % 8 == 0;
+                          Mtot >= ffn_min_rows && cur_a.ld == src_a.ld && cur_a.ld % 8 == 0;
     if (ffn_norm) {
       FfnParams q{};
-      q.M = (int)M; q.H = W.ff_in[2].N;
-      q.X = cur_a.h; q.ldx = cur_a.ld;
+      q.H = W.ff_in[2].N; q.nseg = 1;
+      FfnSeg& g = q.seg[0];
+      g.M = (int)M; g.X = cur_a.h; q.ldx = cur_a.ld;
       q.W1f = W.ffn_w1f[2]; q.b1 = W.ff_in[2].b; q.W2f = W.ffn_w2f[2]; q.b2 = W.ff_out[2].b;
-      q.resid = cur; q.orig = src; q.C = src; q.ldc = D;
-      q.Ch = src_a.h; q.Cl = src_a.l; q.ldch = src_a.ld;
+      g.resid = cur; g.orig = src; g.C = src; q.ldc = D;
+      g.Ch = src_a.h; g.Cl = src_a.l; q.ldch = src_a.ld;
       q.byp = W.bypass; q.nb = W.norm_bias; q.log_scale = W.norm_log_scale;
-      q.rowvec = temb; q.rowvec_ld = D; q.rows_per_group = L;
-      q.C2h = has_next ? cur_a.h : nullptr; q.C2l = has_next ? cur_a.l : nullptr;
-      q.C2 = (has_next && !ff1_src) ? cur : nullptr;
-      launch_ffn(q, s, "ffn_norm_bf16");
+      g.rowvec = temb; q.rowvec_ld = D; q.rows_per_group = L;
+      g.C2h = has_next ? cur_a.h : nullptr; g.C2l = has_next ? cur_a.l : nullptr;
+      g.C2 = (has_next && !ff1_src) ? cur : nullptr;
+      ffn_site(q, ws, s, "ffn_norm_bf16");
     } else {                                          // FF3: only the fp32 stream feeds BiasNorm
       Out e = res;                                    // (which rewrites both copies): no bf16 copy
       if (!pairm) e.act = Act{};
@@ -1384,17 +1573,24 @@ struct zv_engine {
     // Independent row blocks on their own streams (rows never interact on this path): the
     // kernels of one block (GEMMs: MFMA/LDS) co-run with another block's (attention: VALU;
     // epilogues: HBM) instead of the whole batch passing each kernel in lock step.
-    // Bitwise equal to the single-stream decoder (tests/test_gpu_split_streams.py).
+    // Bitwise equal to the single-stream decoder (tests/test_gpu_split_streams.py): every kernel
+    // choice that depends on a row count takes the batch's (dec_rows_N), not the row block's, and
+    // the FeedForward modules run as one launch over all row blocks (run_joined).
     const int parts = std::min(split_streams, std::min(N, MAX_SPLIT));
     if (!split_fork) {
       ZV_CHECK(hipEventCreateWithFlags(&split_fork, hipEventDisableTiming));
       for (int i = 0; i < MAX_SPLIT - 1; ++i) {
-        split_stream[i] = pooled_stream(i);
+        split_stream[i] = engine_stream(i);
         ZV_CHECK(hipEventCreateWithFlags(&split_join[i], hipEventDisableTiming));
       }
     }
     const int outN = dec.out_proj[sidx].N;
     ZV_CHECK(hipEventRecord(split_fork, s));
+    // the joined FeedForward (ffn_site) needs the row blocks' host code interleaved: coroutines
+    // on this thread (also under stream capture: the joins are event dependencies of the graph,
+    // and the warm-up run that sizes the workspace took the same path)
+    const bool join = ffn_join && ffn_fused;
+    std::vector<std::function<void()>> fns;
     int r0 = 0;
     for (int i = 0; i < parts; ++i) {
       const int n = N / parts + (i < N % parts ? 1 : 0);
@@ -1404,10 +1600,28 @@ struct zv_engine {
       if (xin.l) xi.l += rows * xin.ld;
       hipStream_t si = i == 0 ? s : split_stream[i - 1];
       if (i > 0) ZV_CHECK(hipStreamWaitEvent(si, split_fork, 0));
-      decoder_rows(i == 0 ? ws_dec : ws_split[i - 1], xi, sidx, n, T, pad ? pad + rows : nullptr,
-                   t + r0, g ? g + r0 : nullptr, out + rows * outN, si);
+      Workspace* wsi = i == 0 ? &ws_dec : &ws_split[i - 1];
+      const uint8_t* padi = pad ? pad + rows : nullptr;
+      const float* ti = t + r0;
+      const float* gi = g ? g + r0 : nullptr;
+      float* oi = out + rows * outN;
+      fns.push_back([this, wsi, xi, sidx, n, T, padi, ti, gi, oi, si]() {
+        decoder_rows(*wsi, xi, sidx, n, T, padi, ti, gi, oi, si);
+      });
       r0 += n;
     }
+    dec_rows_N = N;   // every row block makes the batch's fused / unfused FeedForward choice
+    dec_parts = join ? 0 : parts;
+    try {
+      if (join) run_joined(fns);
+      else for (auto& f : fns) f();
+    } catch (...) {
+      dec_rows_N = 0;
+      dec_parts = 0;
+      throw;
+    }
+    dec_rows_N = 0;
+    dec_parts = 0;
     for (int i = 1; i < parts; ++i) {
       ZV_CHECK(hipEventRecord(split_join[i - 1], split_stream[i - 1]));
       ZV_CHECK(hipStreamWaitEvent(s, split_join[i - 1], 0));
@@ -1512,7 +1726,7 @@ struct zv_engine {
       return;
     }
     if (!gstream) {
-      gstream = pooled_stream(MAX_SPLIT - 1);
+      gstream = engine_stream(MAX_SPLIT - 1);
       ZV_CHECK(hipEventCreateWithFlags(&gev_in, hipEventDisableTiming));
       ZV_CHECK(hipEventCreateWithFlags(&gev_out, hipEventDisableTiming));
     }
