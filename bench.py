@@ -61,12 +61,16 @@ HBM_PEAK_GBS = 8000.0
 # PMC traffic per launch (tools/pmc_traffic.py) of the kernels the roofline reports, keyed by
 # the engine's profiler tag (one symbol per tag since round 3: the residual linears by ROLE, the
 # fused FeedForward with / without the BiasNorm epilogue); newest measurement first
-TRAFFIC_FILES = {"gemm_bf16_resid": ["r03_gemm_resid_r1_traffic.json", "r02c_gemm_resid_traffic.json"],
-                 "gemm_bf16_resid_rv": ["r03_gemm_resid_r4_traffic.json"],
-                 "gemm_bf16_resid_byp": ["r03_gemm_resid_r2_traffic.json"],
-                 "ffn_bf16": ["r03_ffn_traffic.json"],
-                 "ffn_norm_bf16": ["r03_ffn_norm_traffic.json"],
-                 "gemm_bf16": ["r03_gemm_traffic.json", "r02c_gemm_traffic.json", "r02b_gemm_traffic.json"]}
+# (round 4: measured on the timed three-stream schedule, the same launch set the roofline pass times)
+TRAFFIC_FILES = {"gemm_bf16_resid": ["r04_gemm_resid_r1_traffic.json", "r03_gemm_resid_r1_traffic.json"],
+                 "gemm_bf16_resid_rv": ["r04_gemm_resid_r4_traffic.json", "r03_gemm_resid_r4_traffic.json"],
+                 "gemm_bf16_resid_byp": ["r04_gemm_resid_r2_traffic.json", "r03_gemm_resid_r2_traffic.json"],
+                 "ffn_bf16": ["r04_ffn_traffic.json", "r03_ffn_traffic.json"],
+                 "ffn_norm_bf16": ["r04_ffn_norm_traffic.json", "r03_ffn_norm_traffic.json"],
+                 "ffn_bf16+ffn_norm_bf16": ["r04_ffn_all_traffic.json"],
+                 "gemm_bf16": ["r04_gemm_traffic.json", "r03_gemm_traffic.json"]}
+# the residual-stream linears by epilogue ROLE (zv_gemm.inc): the HBM-bound family of the path
+RESID_TAGS = ("gemm_bf16_resid", "gemm_bf16_resid_rv", "gemm_bf16_resid_byp")
 # analytic FLOPs of one decoder sequence-forward (FlopCounterMode fit on the
 # reference, within 1 %) and of the vocoder per frame
 def decoder_flops(T):
@@ -192,24 +196,28 @@ def _kernel_roofline(name, r, total_ms):
         traffic = t.get("traffic_bytes_per_launch")
         tsrc = (f"profiles/{tfile}: rocprofv3 PMC FETCH_SIZE(x2, gfx950) + WRITE_SIZE "
                 f"per launch of {t['kernel_regex']} over one guided forward")
+    alg = r["bytes"] / r["launches"]
     out = {
         "kernel": name, "bound": "hbm" if hbm else "mfma", "achieved": round(achieved, 2), "peak": peak,
         "unit": unit, "frac": round(achieved / peak, 4), "traffic": traffic,
         "traffic_unit": "bytes per launch", "traffic_source": tsrc,
+        "algorithmic_bytes_per_launch": round(alg),
+        "traffic_over_algorithmic": round(traffic / alg, 3) if traffic else None,
+        "hbm_frac": round(alg / (r["ms"] * 1e-3 / r["launches"]) / 1e9 / HBM_PEAK_GBS, 4),
         "launches_per_step": r["launches"], "avg_launch_us": round(r["ms"] * 1e3 / r["launches"], 2),
         "flops_per_launch": r["flops"] / r["launches"],
         "tflops_achieved": round(r["flops"] / sec / 1e12, 2),
         "share_of_profiled_time": round(r["ms"] / total_ms, 3),
     }
-    if hbm:
-        out["algorithmic_bytes_per_launch"] = r["bytes"] / r["launches"]
     return out
 
 
 def roofline(job):
-    """One extra, untimed step with the engine's per-launch HIP-event profiler on:
-    the dominant kernel's algorithmic work per launch / its average duration (HIP events
-    on the launch stream), plus the same object for the plain GEMM family."""
+    """One extra, untimed step with the engine's per-launch HIP-event profiler on, on the
+    timed schedule (the decoder's three row-block streams: the launch set the rocprofv3
+    summary of the bench command and the PMC traffic files also see): the dominant kernel's
+    algorithmic work per launch / its average duration (HIP events on the launch stream), and
+    the residual-linear family (the HBM-bound one) per epilogue ROLE as `secondary`."""
     from zipvoice_amd import engine
     torch.cuda.synchronize()
     engine.profile(True)
@@ -218,10 +226,18 @@ def roofline(job):
     rep = engine.profile_report()
     engine.profile(False)
     total_ms = sum(v["ms"] for v in rep.values())
-    name, r = max(rep.items(), key=lambda kv: kv[1]["ms"])
+    # the FeedForward kernel is one symbol family over two tags (with / without the BiasNorm
+    # epilogue): the dominant object prices their union
+    ff = [k for k in ("ffn_bf16", "ffn_norm_bf16") if k in rep]
+    if ff:
+        name = "+".join(ff)
+        r = {k: sum(rep[t][k] for t in ff) for k in ("ms", "flops", "bytes", "launches")}
+    else:
+        name, r = max(rep.items(), key=lambda kv: kv[1]["ms"])
     res = _kernel_roofline(name, r, total_ms)
-    if name != "gemm_bf16" and "gemm_bf16" in rep:
-        res["secondary"] = _kernel_roofline("gemm_bf16", rep["gemm_bf16"], total_ms)
+    if len(ff) > 1:
+        res["per_tag"] = {t: _kernel_roofline(t, rep[t], total_ms) for t in ff}
+    res["secondary"] = {t: _kernel_roofline(t, rep[t], total_ms) for t in RESID_TAGS if t in rep}
     res["per_kernel_ms_per_step"] = {k: round(v["ms"], 3) for k, v in rep.items()}
     return res
 

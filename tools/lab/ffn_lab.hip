@@ -7,7 +7,7 @@
 //   seg3     pers with the rows cut into three ranges with their own buffers (bit for bit);
 //   noEpi    pers without the epilogue (ablation).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I zipvoice_amd/csrc tools/lab/ffn_lab.hip -o tools/lab/ffn_lab
-//   ffn_lab [rounds] [mode,...] [MxH;...] [blocks]   modes: 1 residual, 2 + bypass original,
+//   ffn_lab [rounds] [mode,...] [MxH;...] [blocks] [arms]   modes: 1 residual, 2 + bypass original,
 //           4 + row vector, 8 FF3 + BiasNorm epilogue (no unfused arm)
 #include <cstdio>
 #include <cstdlib>
@@ -74,6 +74,8 @@ int main(int argc, char** argv) {
     }
   }
   const int blocks_max = argc > 4 ? atoi(argv[4]) : 0;
+  // arms to time (counter runs time one): a subset of "unfused,classic,pers,seg3,noEpi"
+  const char* arm_sel = argc > 5 ? argv[5] : "unfused,classic,pers,seg3,noEpi";
   hipStream_t s;
   ZV_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   hipEvent_t e0, e1;
@@ -86,6 +88,8 @@ int main(int argc, char** argv) {
   ZV_CHECK(hipMalloc(&err, 16));
   ZV_CHECK(hipMemset(flag, 0, 4096));
   ZV_CHECK(hipMemset(err, 0, 16));
+  unsigned long long* dbg;
+  ZV_CHECK(hipMalloc(&dbg, 1024 * 4 * 6 * 8));
   for (auto& sh : shapes) {
     const int M = sh[0], H = sh[1];
     const long Hp = round_up(H, 256);
@@ -135,6 +139,7 @@ int main(int argc, char** argv) {
         f.H = H; f.nseg = nseg; f.ldx = D; f.ldc = D; f.ldch = D; f.rows_per_group = 1;
         f.W1f = W1f; f.b1 = b1; f.W2f = W2f; f.b2 = b2;
         if (pers) { f.part = part; f.flag = flag; f.err = err; }
+        f.dbg = dbg;
         const int cut[4] = {0, M / 3 + 77, 2 * M / 3 + 5, M};
         for (int i = 0; i < nseg; ++i) {
           const int r0 = nseg == 1 ? 0 : cut[i], r1 = nseg == 1 ? M : cut[i + 1];
@@ -209,6 +214,7 @@ int main(int argc, char** argv) {
       std::vector<float> t[5];
       for (int r = 0; r < rounds; ++r) {
         for (int a = norm ? 1 : 0; a < 5; ++a) {
+          if (!strstr(arm_sel, names[a])) continue;
           auto go = [&]() {
             if (a == 0) unfused();
             else if (a == 1) launch_ffn(fc, s, "lab", blocks_max);
@@ -229,12 +235,28 @@ int main(int argc, char** argv) {
       const double fl = 4.0 * M * D * (double)H;
       printf("   ");
       for (int a = norm ? 1 : 0; a < 5; ++a) {
+        if (t[a].empty()) continue;
         std::vector<float> v = t[a];
         std::sort(v.begin(), v.end());
         const double ms = v[v.size() / 2];
         printf("  %s %.1fus %.0fTF", names[a], ms * 1e3, fl / (ms * 1e-3) / 1e12);
       }
       printf("\n");
+#if FFN_TIMING
+      // the last launch's per-wave clock totals (FFN_TIMING build): where a chunk step goes
+      {
+        const int nb = ffn_schedule(cdiv(M, FFN_BM), H / FFN_HC, blocks_max > 0 ? blocks_max : zv_num_cus(), true).blocks;
+        std::vector<unsigned long long> hd((size_t)nb * 4 * 6);
+        ZV_CHECK(hipMemcpy(hd.data(), dbg, hd.size() * 8, hipMemcpyDeviceToHost));
+        double tot = 0, rt = 0, vm = 0, bar = 0, st = 0;
+        for (int b = 0; b < nb * 4; ++b) {
+          tot += hd[b * 6]; rt += hd[b * 6 + 1]; vm += hd[b * 6 + 2]; bar += hd[b * 6 + 3]; st += hd[b * 6 + 4];
+        }
+        printf("    timing (last launch, per wave): %.0f clk total, %.1f us (%.2f GHz), %.0f steps, per step %.0f clk, "
+               "vmcnt wait %.0f, barrier %.0f\n", tot / (nb * 4), rt / (nb * 4) / 100.0, tot / rt * 0.1,
+               st / (nb * 4), tot / st, vm / st, bar / st);
+      }
+#endif
       fflush(stdout);
     }
     for (void* b : std::initializer_list<void*>{X, W1, W2, W1f, W2f, hid, Ch, Ch2, Ch3, Cl2, Cl3, C2h2, C2h3,

@@ -468,10 +468,10 @@ struct zv_engine {
       return;
     }
     attach_ffn_scratch(q, ws);
-    // a row block's launch on the split decoder: its share of the CUs (the blocks' streams run
-    // their FeedForward modules at about the same time; ZV_FFN_SPLIT_BLOCKS overrides)
-    int bmax = 0;
-    if (dec_parts > 1) bmax = ffn_split_blocks > 0 ? ffn_split_blocks : cdiv(zv_num_cus(), dec_parts);
+    // a row block's launch on the split decoder: lines over every CU (persistent only past one
+    // row block per CU).  ZV_FFN_SPLIT_BLOCKS caps a row block's launch at that many blocks (its
+    // share of the chip: C2 437 ms at 86 blocks, 424 at 128, 417 uncapped, profiles/r04_ffn_ab.txt)
+    const int bmax = (dec_parts > 1 && ffn_split_blocks > 0) ? ffn_split_blocks : 0;
     launch_ffn(q, s, tag, bmax);
   }
   void ffn_join_launch() {
@@ -1524,11 +1524,15 @@ struct zv_engine {
           ZV_LAUNCH_CHECK();
         }
         stack<SPLIT>(Z, S, ws, d, d_a, N, dL, pds, te, s);
-        ZV_REQUIRE(D % 4 == 0 && 256 % (D / 4) == 0, "upsample_combine needs 256 % (D/4) == 0");
-        const long rows_per_block = 4L * (256 / (D / 4));
-        hipLaunchKernelGGL(zv_upsample_combine_kernel,
-                           dim3((unsigned)((M + rows_per_block - 1) / rows_per_block)), dim3(256), 0,
-                           s, main, d, S.combiner, main, N, T, dL, D, S.ds);
+        if (D % 4 == 0 && 256 % (D / 4) == 0) {   // row blocks of whole rows (f32x4 per thread)
+          const long rows_per_block = 4L * (256 / (D / 4));
+          hipLaunchKernelGGL(zv_upsample_combine_kernel,
+                             dim3((unsigned)((M + rows_per_block - 1) / rows_per_block)), dim3(256), 0,
+                             s, main, d, S.combiner, main, N, T, dL, D, S.ds);
+        } else {                                  // any other width (e.g. 384, 192)
+          hipLaunchKernelGGL(zv_upsample_combine_any_kernel, grid1d(M * D), dim3(256), 0, s, main, d,
+                             S.combiner, main, N, T, dL, D, S.ds);
+        }
         ZV_LAUNCH_CHECK();
       }
     }
@@ -1565,8 +1569,9 @@ struct zv_engine {
     if (stereo()) sidx = (Fin == dec.in_proj[0].K) ? 0 : 1;
     ZV_REQUIRE(Fin == dec.in_proj[sidx].K, "decoder input width does not match in_proj");
     io_split = cfg.precision == ZV_MIXED;
-    // (profiled passes run one stream: per-kernel event durations stay per-kernel)
-    if (split_streams < 2 || N < 2 || (long)N * T < split_min_rows || g_zv_prof.on) {
+    // (profiled passes run the same schedule as the timed ones: their per-launch event durations,
+    // the rocprofv3 trace of the bench command and the PMC traffic files describe one launch set)
+    if (split_streams < 2 || N < 2 || (long)N * T < split_min_rows) {
       decoder_rows(ws_dec, xin, sidx, N, T, pad, t, g, out, s);
       return;
     }
