@@ -283,7 +283,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp8"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp16", "fp8"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fp32-mode", action="store_true")
     args = ap.parse_args()

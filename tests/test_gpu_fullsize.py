@@ -94,6 +94,29 @@ def test_velocity_full_size_vs_oracle(name, precision):
     check(v, _refs[name], precision, f"{name} velocity B={B} T={T} t={t} g={g}")
 
 
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_velocity_full_size_fp16_fused_ff(monkeypatch, name):
+    """The fp16 parity mode with the fused FeedForward on every launch (ZV_FFN_MIN_ROWS=0; by
+    default launches of a batch under 10000 rows keep the unfused pair, and these B <= 2 shapes
+    would never reach the kernel the bench runs) at every config's real length, held to
+    north_star's 1e-3 mean bar with no escape."""
+    variant, B, T, lens, Fx, t, g = CASES[name]
+    x, tc, sc, pm = inputs(B, T, Fx, lens, seed=int(name[1:]))
+    monkeypatch.setenv("ZV_FFN_MIN_ROWS", "0")
+    from zipvoice_amd.config import default_config
+    from zipvoice_amd.models import build_model
+    from zipvoice_amd.weights import synthetic_state_dict
+    cfg = default_config(variant)
+    m = build_model(cfg, precision="fp16")
+    m.load_state_dict(synthetic_state_dict(cfg, 0))
+    m = m.to("cuda:0")
+    v = m.engine.velocity(t, g, cuda(x), cuda(tc), cuda(sc), cuda(pm))
+    if name not in _refs:
+        _refs[name] = oracle(variant).velocity(np.float32(t), x, tc, sc, pm, g)
+    check(v, _refs[name], "fp16", f"{name} velocity B={B} T={T} t={t} g={g}, fused FF on every launch")
+    del m
+
+
 def test_c2_batch_rows_equal_single_utterance(monkeypatch):
     """The C2 bench shape (32 utterances = 64 CFG rows, T = 1219, bf16): each row of the
     batched velocity equals the single-utterance run (rows are independent: no

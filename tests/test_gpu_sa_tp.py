@@ -3,13 +3,14 @@
 (zv_attn_sa_kernel, ZV_SA_TP=0) and the oracle.  The two differ only in where the
 positional table is rounded (16-bit operand vs fp32 FMAs) and the summation order, so
 they agree to the 16-bit mode's own resolution.  The default (Toeplitz) form stays inside its
-mode's parity bar against the fp32 oracle (bf16: mean 5e-2; fp16 mixed mode: mean 1e-3); the
-VALU form is an A/B arm, held to 1.25x that bar.  This random input (one velocity at t = 0.4,
-not a fixture) sits at the fp16 mode's 1e-3 bar: 1.06e-3 with the default path since round 3's
-mixed-mode changes (weight-split attention-score projection), so the fp16 case here is held to
-1.2e-3; the mode's parity gate is the fixture suite and the full-size C2-C5 velocities
-(tests/test_gpu_parity.py, test_gpu_fullsize.py: mean < 1e-3, 3e-4 - 8.6e-4).  In the fp16 mode the two arms' own rounding errors (each ~1e-3 against the
-oracle) are independent, so their difference is bounded by the sum of the two bars."""
+mode's parity bar against the fp32 oracle (bf16: mean 5e-2; fp16 parity mode: mean 1e-3, the
+north-star bar, fixed); the VALU form is an A/B arm, held to 1.25x that bar.  This random input
+(one velocity at t = 0.4, not a fixture) sat at 1.06e-3 in the fp16 mode until round 4 made the
+SelfAttention value projection a weight-split product and its out-projection's residual update a
+split product (ZV_MIXED_SA; the emulation puts the input at 8.9e-4 with them,
+profiles/r04_precision_study_r04_velocity_T203.txt); the VALU arm keeps the 16-bit forms.  The
+two arms' own rounding errors are independent, so their difference is bounded by the sum of the
+two bars."""
 import numpy as np
 import pytest
 
@@ -18,7 +19,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.mark.parametrize("precision,bar,ab", [("bf16", 5e-2, 2e-2), ("fp16", 1.2e-3, 2.7e-3)])
+@pytest.mark.parametrize("precision,bar,ab", [("bf16", 5e-2, 2e-2), ("fp16", 1e-3, 2.25e-3)])
 def test_sa_tp_vs_valu_and_oracle(monkeypatch, precision, bar, ab):
     from oracle.zipvoice_np import ZipVoiceOracle
     from zipvoice_amd.config import default_config

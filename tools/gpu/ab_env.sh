@@ -17,7 +17,7 @@ for r in $(seq 1 "$R"); do
   for e in "$@"; do
     i=$((i + 1))
     envs=(); [ "$e" != "-" ] && read -r -a envs <<< "$e"
-    timeout -k 10 300 env "${envs[@]}" python -u bench.py --no-cpu-baseline --no-fp32-mode --steps 4 \
+    timeout -k 10 300 env "${envs[@]}" python -u bench.py --no-cpu-baseline --no-fp32-mode --steps 4 ${BENCH_ARGS:-} \
       > "$O/b_${i}_$r.json" 2> "$O/b_${i}_$r.err" || { echo "bench rc=$? ($e)"; tail -5 "$O/b_${i}_$r.err"; exit 1; }
     python -c "import json;d=json.load(open('$O/b_${i}_$r.json'));print('$e', d['ms_per_step'])" | tee -a "$O/ab.txt"
   done

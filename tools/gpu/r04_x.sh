@@ -5,8 +5,8 @@ cd "${GRAFT_REPO_ROOT:-.}"
 O=gpurun_out/${1:-r04_x}; mkdir -p $O
 for v in t x_noact x_now2 x_now12 x_noact_now12; do
   echo "== $v" >> $O/x.txt
-  timeout -k 10 60 tools/lab/ffn_lab_$v 2 1 "78016x1536" 0 "pers" >> $O/x.txt 2>&1 || { echo "$v rc=$?"; tail -3 $O/x.txt; exit 1; }
+  timeout -k 10 60 tools/lab/ffn_lab_$v 2 1 "78016x1536" 0 "pers,noDMA,noEpi" >> $O/x.txt 2>&1 || { echo "$v rc=$?"; tail -3 $O/x.txt; exit 1; }
 done
 cat $O/x.txt
-timeout -k 10 200 tools/lab/ffn_lab 3 1,2,4,8 "78016x1152;78016x1536;78016x1920;39008x1536;26005x1536" > $O/lab.txt 2>&1 || { echo "lab rc=$?"; tail -5 $O/lab.txt; exit 1; }
+timeout -k 10 200 tools/lab/ffn_lab 3 1,2,4,8 "78016x1152;78016x1536;78016x1920;39008x1536;26005x1536" 0 "unfused,classic,pers,seg3,noEpi" > $O/lab.txt 2>&1 || { echo "lab rc=$?"; tail -5 $O/lab.txt; exit 1; }
 cat $O/lab.txt

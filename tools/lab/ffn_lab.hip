@@ -75,7 +75,7 @@ int main(int argc, char** argv) {
   }
   const int blocks_max = argc > 4 ? atoi(argv[4]) : 0;
   // arms to time (counter runs time one): a subset of "unfused,classic,pers,seg3,noEpi"
-  const char* arm_sel = argc > 5 ? argv[5] : "unfused,classic,pers,seg3,noEpi";
+  const char* arm_sel = argc > 5 ? argv[5] : "unfused,classic,pers,seg3,noEpi,noDMA";
   hipStream_t s;
   ZV_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   hipEvent_t e0, e1;
@@ -210,17 +210,18 @@ int main(int argc, char** argv) {
       const FfnSchedule sc = ffn_schedule(cdiv(M, FFN_BM), nc, blocks_max > 0 ? blocks_max : zv_num_cus(), true);
       printf("  (R %d nc %d w %d blocks %d)\n", cdiv(M, FFN_BM), nc, sc.w, sc.blocks);
       // timing: interleaved rounds, 10 launches per arm per round (no resets: residual in place)
-      const char* names[5] = {"unfused", "classic", "pers", "seg3", "noEpi"};
-      std::vector<float> t[5];
+      const char* names[6] = {"unfused", "classic", "pers", "seg3", "noEpi", "noDMA"};
+      std::vector<float> t[6];
       for (int r = 0; r < rounds; ++r) {
-        for (int a = norm ? 1 : 0; a < 5; ++a) {
+        for (int a = norm ? 1 : 0; a < 6; ++a) {
           if (!strstr(arm_sel, names[a])) continue;
           auto go = [&]() {
             if (a == 0) unfused();
             else if (a == 1) launch_ffn(fc, s, "lab", blocks_max);
             else if (a == 2) launch_ffn(fp, s, "lab", blocks_max);
             else if (a == 3) launch_ffn(f3, s, "lab", blocks_max);
-            else launch_ffn<3>(fp, s, "lab", blocks_max);
+            else if (a == 4) launch_ffn<3>(fp, s, "lab", blocks_max);
+            else launch_ffn<1>(fp, s, "lab", blocks_max);
           };
           go();
           ZV_CHECK(hipEventRecord(e0, s));
@@ -234,7 +235,7 @@ int main(int argc, char** argv) {
       }
       const double fl = 4.0 * M * D * (double)H;
       printf("   ");
-      for (int a = norm ? 1 : 0; a < 5; ++a) {
+      for (int a = norm ? 1 : 0; a < 6; ++a) {
         if (t[a].empty()) continue;
         std::vector<float> v = t[a];
         std::sort(v.begin(), v.end());

@@ -141,11 +141,16 @@ def nonlin_attention(P, x, w0):
 
 
 def self_attention(P, x, W, vdim):
-    prev, EMU.cur = EMU.cur, "sa"
+    # sub-families (round 4; each defaults to "sa"): sa_in the value projection, sa_pv the P and V
+    # operands of P.V, sa_out the out-projection
+    prev = EMU.cur
+    sub = lambda n: n if n in EMU.fam else "sa"  # noqa: E731
     B, L, _ = x.shape
     H = W.shape[0]
+    EMU.cur = sub("sa_in")
     v = linear(x, P["in_proj.weight"], P["in_proj.bias"]).reshape(B, L, H, vdim).transpose(2, 0, 1, 3)
-    o = _pv(W, v, "sa").transpose(1, 2, 0, 3).reshape(B, L, H * vdim)
+    o = _pv(W, v, sub("sa_pv")).transpose(1, 2, 0, 3).reshape(B, L, H * vdim)
+    EMU.cur = sub("sa_out")
     out = linear(o, P["out_proj.weight"], P["out_proj.bias"])
     EMU.cur = prev
     return out
@@ -202,6 +207,9 @@ def main():
     ap.add_argument("--fixture", default="sample_c1.npz")
     ap.add_argument("--mixed", action="store_true")
     ap.add_argument("--r03", action="store_true")
+    ap.add_argument("--velocity", action="store_true",
+                    help="round 4: one guided velocity on the random input of tests/test_gpu_ffn.py "
+                         "(B=2, T=203, lens 203/150, t=0.4, g=1, seed 11) against the exact oracle")
     args = ap.parse_args()
     from zipvoice_amd.config import default_config
     from zipvoice_amd.weights import synthetic_state_dict
@@ -211,6 +219,32 @@ def main():
     o = Z.ZipVoiceOracle(cfg, synthetic_state_dict(cfg, 0))
     KEYS.update({id(v): k for k, v in o.sd.items()})
     fams = ["attn", "qk", "ff", "na", "sa", "conv", "io"]
+    if args.velocity:
+        base = {g: "fp16" for g in fams}
+        mixed = dict(base, io=None, attn="a16")           # the engine's fp16 parity mode (r03)
+        arms = [("fp16 parity mode (io fp32, attn a16, +text fp32)", mixed, True)]
+        for g in ("qk", "ff", "na", "sa", "conv", "sa_in", "sa_pv", "sa_out"):
+            arms.append((f"parity mode, {g} exact", dict(mixed, **{g: None}), True))
+        arms.append(("parity mode, sa_pv + qk exact", dict(mixed, sa_pv=None, qk=None), True))
+        arms.append(("parity mode, sa_in + sa_out exact", dict(mixed, sa_in=None, sa_out=None), True))
+        arms.append(("parity mode, sa_out exact + sa_in a16", dict(mixed, sa_in="a16", sa_out=None), True))
+        arms.append(("parity mode, sa_out w16 + sa_in a16", dict(mixed, sa_in="a16", sa_out="w16"), True))
+        arms.append(("parity mode, sa + qk exact", dict(mixed, sa=None, qk=None), True))
+        arms.append(("parity mode, sa_out + qk exact", dict(mixed, sa_out=None, qk=None), True))
+        arms.append(("parity mode, na + sa_out exact", dict(mixed, na=None, sa_out=None), True))
+        cand = dict(mixed, sa_in="a16", sa_out=None)
+        arms.append(("cand: sa_in a16 + sa_out exact, io fp16", dict(cand, io="fp16"), True))
+        arms.append(("cand: sa_in a16 + sa_out exact, io a16", dict(cand, io="a16"), True))
+        arms.append(("cand: sa_in a16 + sa_out exact, io w16", dict(cand, io="w16"), True))
+        arms.append(("cand: sa_in a16 + sa_out exact, attn fp16", dict(cand, attn="fp16"), True))
+        arms.append(("cand: sa_in a16 + sa_out exact, text fp16", cand, False))
+        arms.append(("parity mode, sa_out a16 (W split)", dict(mixed, sa_out="a16"), True))
+        arms.append(("parity mode, sa_out w16 (A split)", dict(mixed, sa_out="w16"), True))
+        arms.append(("parity mode, sa_in a16 (W split)", dict(mixed, sa_in="a16"), True))
+        arms.append(("parity mode, attn exact", dict(mixed, attn=None), True))
+        arms.append(("parity mode, text fp16", mixed, False))
+        run_velocity(o, cfg, arms, args.out.replace(".txt", "_r04_velocity_T203.txt"))
+        return
     if "--r03" in sys.argv:
         # cheaper parity-grade candidates: one-sided split products for the attention-score
         # projection, and dropping the text-encoder / in-out splits
@@ -249,6 +283,30 @@ def main():
             arms.append((f"{'+'.join(keep)} fp32, rest {fmt}",
                          {g: (None if g in keep else fmt) for g in fams}))
     run_arms(o, d, [(n, f, False) for n, f in arms], args.out)
+
+
+def run_velocity(o, cfg, arms, out):
+    rng = np.random.default_rng(11)
+    B, T = 2, 203
+    x = rng.standard_normal((B, T, cfg.feat_dim), dtype=np.float32)
+    tc = rng.standard_normal(x.shape, dtype=np.float32)
+    sc = rng.standard_normal(x.shape, dtype=np.float32)
+    pm = np.arange(T)[None] >= np.array([203, 150])[:, None]
+    EMU.fam, EMU.text_exact = {}, True
+    ref = o.velocity(np.float32(0.4), x, tc, sc, pm, 1.0)
+    lines = ["# precision study (round 4): oracle with emulated MFMA-operand rounding; one guided "
+             "velocity on tests/test_gpu_ffn.py's random input (B=2, T=203, lens 203/150, t=0.4, g=1, "
+             "seed 11); metric = mean / max |v - exact oracle| over valid frames"]
+    for name, fam, tx in arms:
+        EMU.fam, EMU.text_exact = fam, tx
+        t0 = time.time()
+        v = o.velocity(np.float32(0.4), x, tc, sc, pm, 1.0)
+        e = np.abs(v - ref)[~pm]
+        line = f"{name:50s} mean {e.mean():.3e} max {e.max():.3e}   ({time.time() - t0:.1f} s)"
+        print(line, flush=True)
+        lines.append(line)
+    with open(out, "w") as f:
+        f.write("\n".join(lines) + "\n")
 
 
 def run_arms(o, d, arms, out):
