@@ -112,6 +112,14 @@ int64_t zv_device_bytes(zv_handle h);
 int zv_profile(int enable);
 int zv_profile_report(char* buf, int buflen);
 
+/* Number of host-blocking HIP runtime calls the library has issued since load (process-wide:
+ * allocations, frees, synchronous copies / memsets, device / stream / event synchronisation,
+ * stream / event / graph creation and destruction).  A warm zv_euler_sample /
+ * zv_vocoder_decode at an already-seen shape adds none: the per-rank step never waits on the
+ * GPU inside the Euler loop (no reference counterpart: the reference's solver loop,
+ * zipvoice/models/modules/solver.py:213-240, runs eagerly on the caller's stream). */
+int64_t zv_host_block_count(void);
+
 /* GEMM microbenchmark (random bf16 operands): average ms per launch of tile
  * variant `variant` (+100: one tile per block instead of the persistent grid) for
  * C(M,N) = A(M,K) W(N,K)^T with out_mode 0 = fp32 C, 1 = bf16 C, 2 = residual

@@ -42,6 +42,16 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
                                " at " __FILE__ ":" + std::to_string(__LINE__) + ": " #expr); \
   } while (0)
 
+// Host-blocking runtime calls (allocation and free, synchronous copies and memsets, device /
+// stream / event synchronisation, stream / event / graph creation and destruction, copies to
+// pageable host memory) are issued as ZV_BLOCKING(call): it counts them (zv_host_block_count in
+// the C ABI) so a test can assert that a warm sample() issues none between its entry and its
+// return (tests/test_gpu_host_sync.py); tests/test_host_block_scan.py checks on the CPU that no
+// such call in csrc/ bypasses the counter.
+#include <atomic>
+static std::atomic<long long> g_zv_host_blocks{0};
+#define ZV_BLOCKING(call) (g_zv_host_blocks.fetch_add(1, std::memory_order_relaxed), (call))
+
 #define ZV_REQUIRE(cond, msg)                                                           \
   do {                                                                                  \
     if (!(cond)) throw std::invalid_argument(std::string(msg));                         \
@@ -154,8 +164,8 @@ struct ZvProfScope {
       : s(st), active(g_zv_prof.on) {
     if (active) {
       rec.name = name; rec.flops = flops; rec.bytes = bytes;
-      (void)hipEventCreate(&rec.e0);
-      (void)hipEventCreate(&rec.e1);
+      (void)ZV_BLOCKING(hipEventCreate(&rec.e0));
+      (void)ZV_BLOCKING(hipEventCreate(&rec.e1));
       (void)hipEventRecord(rec.e0, s);
     }
   }

@@ -112,17 +112,17 @@ struct DBuf {
     size_t need = n * sizeof(T) + 256;
     if (need > bytes) {
       ++g_ws_generation;
-      if (p) { ZV_CHECK(hipDeviceSynchronize()); ZV_CHECK(hipFree(p)); }
-      ZV_CHECK(hipMalloc(&p, need));
-      ZV_CHECK(hipMemset(p, 0, need));
+      if (p) { ZV_CHECK(ZV_BLOCKING(hipDeviceSynchronize())); ZV_CHECK(ZV_BLOCKING(hipFree(p))); }
+      ZV_CHECK(ZV_BLOCKING(hipMalloc(&p, need)));
+      ZV_CHECK(ZV_BLOCKING(hipMemset(p, 0, need)));
       // the memset runs on the null stream, which does not order against the engine's
       // non-blocking streams (graph / split-decoder streams): finish it before any use
-      ZV_CHECK(hipDeviceSynchronize());
+      ZV_CHECK(ZV_BLOCKING(hipDeviceSynchronize()));
       bytes = need;
     }
     return reinterpret_cast<T*>(p);
   }
-  ~DBuf() { if (p) (void)hipFree(p); }
+  ~DBuf() { if (p) (void)ZV_BLOCKING(hipFree(p)); }
 };
 
 struct Act {           // GEMM operand in HBM: bf16 hi (+ lo in fp32-accurate mode)
@@ -203,12 +203,12 @@ static StreamSet acquire_stream_set() {
   }
   StreamSet set;
   set.dev = dev;
-  for (auto& st : set.s) ZV_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  for (auto& st : set.s) ZV_CHECK(ZV_BLOCKING(hipStreamCreateWithFlags(&st, hipStreamNonBlocking)));
   return set;
 }
 static void release_stream_set(const StreamSet& set) {
   if (set.dev < 0) return;
-  for (hipStream_t st : set.s) (void)hipStreamSynchronize(st);
+  for (hipStream_t st : set.s) (void)ZV_BLOCKING(hipStreamSynchronize(st));
   std::lock_guard<std::mutex> lock(g_stream_pool_mu);
   stream_pool_free().push_back(set);
 }
@@ -506,8 +506,8 @@ struct zv_engine {
     co.n = (int)fns.size();
     co.abort = false;
     if (!co.ev_done) {
-      ZV_CHECK(hipEventCreateWithFlags(&co.ev_done, hipEventDisableTiming));
-      for (int i = 0; i < MAX_SPLIT; ++i) ZV_CHECK(hipEventCreateWithFlags(&co.ev_ready[i], hipEventDisableTiming));
+      ZV_CHECK(ZV_BLOCKING(hipEventCreateWithFlags(&co.ev_done, hipEventDisableTiming)));
+      for (int i = 0; i < MAX_SPLIT; ++i) ZV_CHECK(ZV_BLOCKING(hipEventCreateWithFlags(&co.ev_ready[i], hipEventDisableTiming)));
     }
     for (int i = 0; i < co.n; ++i) {
       FfnCo::Part& pt = co.part[i];
@@ -559,7 +559,7 @@ struct zv_engine {
   }
 
   void drop_graphs() {
-    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second.exec);
+    for (auto& kv : graphs) (void)ZV_BLOCKING(hipGraphExecDestroy(kv.second.exec));
     graphs.clear();
   }
   void evict_lru_graph() {
@@ -567,8 +567,8 @@ struct zv_engine {
     for (auto it = graphs.begin(); it != graphs.end(); ++it)
       if (it->second.last_use < victim->second.last_use) victim = it;
     // its last replay may still run on gstream: destroy only after it drained
-    ZV_CHECK(hipStreamSynchronize(gstream));
-    ZV_CHECK(hipGraphExecDestroy(victim->second.exec));
+    ZV_CHECK(ZV_BLOCKING(hipStreamSynchronize(gstream)));
+    ZV_CHECK(ZV_BLOCKING(hipGraphExecDestroy(victim->second.exec)));
     graphs.erase(victim);
   }
 
@@ -583,21 +583,21 @@ struct zv_engine {
     drop_graphs();
     // the stream set outlives the engine: drain what this engine queued on it, then return it
     release_stream_set(streams);
-    if (gev_in) (void)hipEventDestroy(gev_in);
-    if (gev_out) (void)hipEventDestroy(gev_out);
+    if (gev_in) (void)ZV_BLOCKING(hipEventDestroy(gev_in));
+    if (gev_out) (void)ZV_BLOCKING(hipEventDestroy(gev_out));
     for (int i = 0; i < MAX_SPLIT - 1; ++i)
-      if (split_join[i]) (void)hipEventDestroy(split_join[i]);
-    if (split_fork) (void)hipEventDestroy(split_fork);
+      if (split_join[i]) (void)ZV_BLOCKING(hipEventDestroy(split_join[i]));
+    if (split_fork) (void)ZV_BLOCKING(hipEventDestroy(split_fork));
     for (int i = 0; i < MAX_SPLIT; ++i)
-      if (co.ev_ready[i]) (void)hipEventDestroy(co.ev_ready[i]);
-    if (co.ev_done) (void)hipEventDestroy(co.ev_done);
-    for (void* p : allocs) (void)hipFree(p);
+      if (co.ev_ready[i]) (void)ZV_BLOCKING(hipEventDestroy(co.ev_ready[i]));
+    if (co.ev_done) (void)ZV_BLOCKING(hipEventDestroy(co.ev_done));
+    for (void* p : allocs) (void)ZV_BLOCKING(hipFree(p));
   }
 
   // ---------------------------------------------------------------- weights
   template <typename T> T* dalloc(size_t n) {
     void* p = nullptr;
-    ZV_CHECK(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)));
+    ZV_CHECK(ZV_BLOCKING(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T))));
     allocs.push_back(p);
     weight_bytes += n * sizeof(T);
     return reinterpret_cast<T*>(p);
@@ -613,7 +613,7 @@ struct zv_engine {
   float* upload_f32(const std::string& k, size_t numel) {
     const auto& v = take(k, numel);
     float* d = dalloc<float>(numel);
-    ZV_CHECK(hipMemcpy(d, v.data(), numel * sizeof(float), hipMemcpyHostToDevice));
+    ZV_CHECK(ZV_BLOCKING(hipMemcpy(d, v.data(), numel * sizeof(float), hipMemcpyHostToDevice)));
     return d;
   }
   // perm (optional): row n of the device matrix is row perm[n] of the reference weight
@@ -635,8 +635,8 @@ struct zv_engine {
       }
     L.hi = dalloc<bf16>(hi.size());
     L.lo = dalloc<bf16>(lo.size());
-    ZV_CHECK(hipMemcpy(L.hi, hi.data(), hi.size() * sizeof(bf16), hipMemcpyHostToDevice));
-    ZV_CHECK(hipMemcpy(L.lo, lo.data(), lo.size() * sizeof(bf16), hipMemcpyHostToDevice));
+    ZV_CHECK(ZV_BLOCKING(hipMemcpy(L.hi, hi.data(), hi.size() * sizeof(bf16), hipMemcpyHostToDevice)));
+    ZV_CHECK(ZV_BLOCKING(hipMemcpy(L.lo, lo.data(), lo.size() * sizeof(bf16), hipMemcpyHostToDevice)));
     if (fp8 && cfg.precision == ZV_FP8 && K % MX8_KSTEP == 0) {
       // MX-fp8 copy of the (permuted) fp32 weight, rows zero-padded to Npad
       L.Kq = K;
@@ -647,12 +647,12 @@ struct zv_engine {
       mx8_quantize_host(wp.data(), K, L.Npad, K, q.data(), K, sc.data());
       L.q8 = dalloc<uint8_t>(q.size());
       L.s8 = dalloc<uint8_t>(sc.size());
-      ZV_CHECK(hipMemcpy(L.q8, q.data(), q.size(), hipMemcpyHostToDevice));
-      ZV_CHECK(hipMemcpy(L.s8, sc.data(), sc.size(), hipMemcpyHostToDevice));
+      ZV_CHECK(ZV_BLOCKING(hipMemcpy(L.q8, q.data(), q.size(), hipMemcpyHostToDevice)));
+      ZV_CHECK(ZV_BLOCKING(hipMemcpy(L.s8, sc.data(), sc.size(), hipMemcpyHostToDevice)));
     }
     if (keep_f32) {
       L.w32 = dalloc<float>((size_t)N * K);
-      ZV_CHECK(hipMemcpy(L.w32, w.data(), (size_t)N * K * sizeof(float), hipMemcpyHostToDevice));
+      ZV_CHECK(ZV_BLOCKING(hipMemcpy(L.w32, w.data(), (size_t)N * K * sizeof(float), hipMemcpyHostToDevice)));
     }
     if (bias) {
       if (perm) {
@@ -660,7 +660,7 @@ struct zv_engine {
         std::vector<float> pb(N);
         for (int n = 0; n < N; ++n) pb[n] = b[(*perm)[n]];
         L.b = dalloc<float>(N);
-        ZV_CHECK(hipMemcpy(L.b, pb.data(), N * sizeof(float), hipMemcpyHostToDevice));
+        ZV_CHECK(ZV_BLOCKING(hipMemcpy(L.b, pb.data(), N * sizeof(float), hipMemcpyHostToDevice)));
       } else {
         L.b = upload_f32(prefix + ".bias", N);
       }
@@ -694,14 +694,14 @@ struct zv_engine {
       }
     L.hi = dalloc<bf16>(hi.size());
     L.lo = dalloc<bf16>(lo.size());
-    ZV_CHECK(hipMemcpy(L.hi, hi.data(), hi.size() * sizeof(bf16), hipMemcpyHostToDevice));
-    ZV_CHECK(hipMemcpy(L.lo, lo.data(), lo.size() * sizeof(bf16), hipMemcpyHostToDevice));
+    ZV_CHECK(ZV_BLOCKING(hipMemcpy(L.hi, hi.data(), hi.size() * sizeof(bf16), hipMemcpyHostToDevice)));
+    ZV_CHECK(ZV_BLOCKING(hipMemcpy(L.lo, lo.data(), lo.size() * sizeof(bf16), hipMemcpyHostToDevice)));
     const auto& ba = take(pa + ".bias", N);
     const auto& bb = take(pb + ".bias", N);
     std::vector<float> b(N);
     for (int n = 0; n < N; ++n) b[n] = ba[n] + bb[n];
     L.b = dalloc<float>(N);
-    ZV_CHECK(hipMemcpy(L.b, b.data(), N * sizeof(float), hipMemcpyHostToDevice));
+    ZV_CHECK(ZV_BLOCKING(hipMemcpy(L.b, b.data(), N * sizeof(float), hipMemcpyHostToDevice)));
     return L;
   }
   // NonlinAttention in_proj rows [s | x | y] -> groups of 48 = [s16 | x16 | y16]
@@ -765,7 +765,7 @@ struct zv_engine {
         for (int k = 0; k < S.ds; ++k) { w[k] = expf(b[k] - mx); sum += w[k]; }
         for (int k = 0; k < S.ds; ++k) w[k] /= sum;
         S.ds_w = dalloc<float>(S.ds);
-        ZV_CHECK(hipMemcpy(S.ds_w, w.data(), S.ds * sizeof(float), hipMemcpyHostToDevice));
+        ZV_CHECK(ZV_BLOCKING(hipMemcpy(S.ds_w, w.data(), S.ds * sizeof(float), hipMemcpyHostToDevice)));
         S.combiner = upload_f32(sp + "out_combiner.bypass_scale", dim);
       }
       if (temb_dim > 0) S.time_emb = make_small(ep + "time_emb.1", dim, temb_dim, true);
@@ -778,7 +778,7 @@ struct zv_engine {
         {
           const auto& pw = take(lp + "self_attn_weights.linear_pos.weight", pw_n);
           W.pos_w = S.pos_w_all + li * pw_n;
-          ZV_CHECK(hipMemcpy(W.pos_w, pw.data(), pw_n * sizeof(float), hipMemcpyHostToDevice));
+          ZV_CHECK(ZV_BLOCKING(hipMemcpy(W.pos_w, pw.data(), pw_n * sizeof(float), hipMemcpyHostToDevice)));
         }
         for (int a = 0; a < 2; ++a) {
           std::string ap = lp + "self_attn" + std::to_string(a + 1) + ".";
@@ -800,7 +800,7 @@ struct zv_engine {
             hipLaunchKernelGGL(zv_ffn_pack_w2_kernel, dim3(cdiv(n, 256)), dim3(256), 0, 0, W.ff_out[f].hi,
                                (long)W.ff_out[f].Kpad, hs[f], W.ffn_w2f[f]);
             ZV_LAUNCH_CHECK();
-            ZV_CHECK(hipDeviceSynchronize());
+            ZV_CHECK(ZV_BLOCKING(hipDeviceSynchronize()));
           }
         }
         const int hid = 3 * dim / 4;
@@ -868,7 +868,7 @@ struct zv_engine {
     for (int k = 0; k < half; ++k)
       fr[k] = expf((float)(-log(10000.0)) * (float)k / (float)half);
     temb_freqs = dalloc<float>(half);
-    ZV_CHECK(hipMemcpy(temb_freqs, fr.data(), half * sizeof(float), hipMemcpyHostToDevice));
+    ZV_CHECK(ZV_BLOCKING(hipMemcpy(temb_freqs, fr.data(), half * sizeof(float), hipMemcpyHostToDevice)));
     // strict=True: nothing left over
     size_t expected = count_expected();
     if (expected != staged.size())
@@ -1605,10 +1605,10 @@ struct zv_engine {
     // the FeedForward modules run as one launch over all row blocks (run_joined).
     const int parts = std::min(split_streams, std::min(N, MAX_SPLIT));
     if (!split_fork) {
-      ZV_CHECK(hipEventCreateWithFlags(&split_fork, hipEventDisableTiming));
+      ZV_CHECK(ZV_BLOCKING(hipEventCreateWithFlags(&split_fork, hipEventDisableTiming)));
       for (int i = 0; i < MAX_SPLIT - 1; ++i) {
         split_stream[i] = engine_stream(i);
-        ZV_CHECK(hipEventCreateWithFlags(&split_join[i], hipEventDisableTiming));
+        ZV_CHECK(ZV_BLOCKING(hipEventCreateWithFlags(&split_join[i], hipEventDisableTiming)));
       }
     }
     const int outN = dec.out_proj[sidx].N;
@@ -1754,8 +1754,8 @@ struct zv_engine {
     }
     if (!gstream) {
       gstream = engine_stream(MAX_SPLIT - 1);
-      ZV_CHECK(hipEventCreateWithFlags(&gev_in, hipEventDisableTiming));
-      ZV_CHECK(hipEventCreateWithFlags(&gev_out, hipEventDisableTiming));
+      ZV_CHECK(ZV_BLOCKING(hipEventCreateWithFlags(&gev_in, hipEventDisableTiming)));
+      ZV_CHECK(ZV_BLOCKING(hipEventCreateWithFlags(&gev_out, hipEventDisableTiming)));
     }
     ZV_CHECK(hipEventRecord(gev_in, s));
     ZV_CHECK(hipStreamWaitEvent(gstream, gev_in, 0));
@@ -1774,14 +1774,14 @@ struct zv_engine {
         euler_loop(sx, stc, ssc, spad, B, T, ts, g, sgr, cfg_rows, gstream);
       } catch (...) {
         (void)hipStreamEndCapture(gstream, &graph);
-        if (graph) (void)hipGraphDestroy(graph);
+        if (graph) (void)ZV_BLOCKING(hipGraphDestroy(graph));
         throw;
       }
       ZV_CHECK(hipStreamEndCapture(gstream, &graph));
       ZV_REQUIRE(gen0 == g_ws_generation, "workspace moved during graph capture");
       hipGraphExec_t exec = nullptr;
-      ZV_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-      ZV_CHECK(hipGraphDestroy(graph));
+      ZV_CHECK(ZV_BLOCKING(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0)));
+      ZV_CHECK(ZV_BLOCKING(hipGraphDestroy(graph)));
       it = graphs.emplace(key, GraphEntry{exec, 0}).first;
     }
     it->second.last_use = ++graph_clock;
@@ -1863,16 +1863,16 @@ static __global__ void zv_fill_rand_bf16(bf16* p, long n, unsigned seed) {
 template <int BM, int BN, int WGM, int WGN, int STAGES, int BK = GEMM_BK, int DEFER = 0, int ROLE = 0>
 static float bench_variant(GemmParams p, int iters, bool persistent, hipStream_t s) {
   hipEvent_t e0, e1;
-  ZV_CHECK(hipEventCreate(&e0)); ZV_CHECK(hipEventCreate(&e1));
+  ZV_CHECK(ZV_BLOCKING(hipEventCreate(&e0))); ZV_CHECK(ZV_BLOCKING(hipEventCreate(&e1)));
   launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES, 2, BK, DEFER, 0, 0, ROLE>(p, 1, s, "bench", persistent);
   ZV_CHECK(hipEventRecord(e0, s));
   for (int i = 0; i < iters; ++i)
     launch_gemm<BM, BN, WGM, WGN, 1, EPI_STD, STAGES, 2, BK, DEFER, 0, 0, ROLE>(p, 1, s, "bench", persistent);
   ZV_CHECK(hipEventRecord(e1, s));
-  ZV_CHECK(hipEventSynchronize(e1));
+  ZV_CHECK(ZV_BLOCKING(hipEventSynchronize(e1)));
   float ms = 0.f;
   ZV_CHECK(hipEventElapsedTime(&ms, e0, e1));
-  ZV_CHECK(hipEventDestroy(e0)); ZV_CHECK(hipEventDestroy(e1));
+  ZV_CHECK(ZV_BLOCKING(hipEventDestroy(e0))); ZV_CHECK(ZV_BLOCKING(hipEventDestroy(e1)));
   return ms / iters;
 }
 
@@ -1880,15 +1880,15 @@ static float bench_variant(GemmParams p, int iters, bool persistent, hipStream_t
 template <int BM, int BN, int WGM, int WGN, int EPI, int STAGES = 2>
 static float bench_variant_pp(GemmParams p, int iters, hipStream_t s) {
   hipEvent_t e0, e1;
-  ZV_CHECK(hipEventCreate(&e0)); ZV_CHECK(hipEventCreate(&e1));
+  ZV_CHECK(ZV_BLOCKING(hipEventCreate(&e0))); ZV_CHECK(ZV_BLOCKING(hipEventCreate(&e1)));
   launch_gemm_pp<BM, BN, WGM, WGN, EPI, 0, STAGES>(p, s, "bench");
   ZV_CHECK(hipEventRecord(e0, s));
   for (int i = 0; i < iters; ++i) launch_gemm_pp<BM, BN, WGM, WGN, EPI, 0, STAGES>(p, s, "bench");
   ZV_CHECK(hipEventRecord(e1, s));
-  ZV_CHECK(hipEventSynchronize(e1));
+  ZV_CHECK(ZV_BLOCKING(hipEventSynchronize(e1)));
   float ms = 0.f;
   ZV_CHECK(hipEventElapsedTime(&ms, e0, e1));
-  ZV_CHECK(hipEventDestroy(e0)); ZV_CHECK(hipEventDestroy(e1));
+  ZV_CHECK(ZV_BLOCKING(hipEventDestroy(e0))); ZV_CHECK(ZV_BLOCKING(hipEventDestroy(e1)));
   return ms / iters;
 }
 #endif
@@ -1948,14 +1948,14 @@ int zv_reserve(zv_handle h, int max_batch, int max_frames) {
   const size_t nt = (size_t)max_batch * max_frames * h->cfg.feat_dim;
   float *x = nullptr, *tc = nullptr, *v = nullptr;
   uint8_t* pad = nullptr;
-  ZV_CHECK(hipMalloc(&x, nx * 4));
-  ZV_CHECK(hipMalloc(&tc, nt * 4));
-  ZV_CHECK(hipMalloc(&v, nx * 4));
-  ZV_CHECK(hipMalloc(&pad, (size_t)max_batch * max_frames));
-  ZV_CHECK(hipMemset(x, 0, nx * 4));
-  ZV_CHECK(hipMemset(tc, 0, nt * 4));
-  ZV_CHECK(hipMemset(pad, 0, (size_t)max_batch * max_frames));
-  auto release = [&]() { (void)hipFree(x); (void)hipFree(tc); (void)hipFree(v); (void)hipFree(pad); };
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&x, nx * 4)));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&tc, nt * 4)));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&v, nx * 4)));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&pad, (size_t)max_batch * max_frames)));
+  ZV_CHECK(ZV_BLOCKING(hipMemset(x, 0, nx * 4)));
+  ZV_CHECK(ZV_BLOCKING(hipMemset(tc, 0, nt * 4)));
+  ZV_CHECK(ZV_BLOCKING(hipMemset(pad, 0, (size_t)max_batch * max_frames)));
+  auto release = [&]() { (void)ZV_BLOCKING(hipFree(x)); (void)ZV_BLOCKING(hipFree(tc)); (void)ZV_BLOCKING(hipFree(v)); (void)ZV_BLOCKING(hipFree(pad)); };
   // the graph path's staging copies of the inputs, too
   (void)h->gx.get<float>(nx);
   (void)h->gtc.get<float>(nt);
@@ -1965,7 +1965,7 @@ int zv_reserve(zv_handle h, int max_batch, int max_frames) {
   try {
     h->velocity(0.25f, 1.0f, nullptr, false, x, tc, x, pad, max_batch, max_frames, v, false,
                 0.f, nullptr);
-    ZV_CHECK(hipDeviceSynchronize());
+    ZV_CHECK(ZV_BLOCKING(hipDeviceSynchronize()));
   } catch (...) {
     release();
     throw;
@@ -1976,7 +1976,7 @@ int zv_reserve(zv_handle h, int max_batch, int max_frames) {
 
 int zv_profile(int enable) {
   ZV_API_BEGIN
-  for (auto& r : g_zv_prof.recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
+  for (auto& r : g_zv_prof.recs) { (void)ZV_BLOCKING(hipEventDestroy(r.e0)); (void)ZV_BLOCKING(hipEventDestroy(r.e1)); }
   g_zv_prof.recs.clear();
   g_zv_prof.on = enable != 0;
   g_zv_prof.detail = enable == 2;
@@ -1989,7 +1989,7 @@ int zv_profile_report(char* buf, int buflen) {
   struct Agg { int n = 0; double flops = 0, bytes = 0, ms = 0; };
   std::map<std::string, Agg> agg;
   for (auto& r : g_zv_prof.recs) {
-    ZV_CHECK(hipEventSynchronize(r.e1));
+    ZV_CHECK(ZV_BLOCKING(hipEventSynchronize(r.e1)));
     float ms = 0.f;
     ZV_CHECK(hipEventElapsedTime(&ms, r.e0, r.e1));
     Agg& a = agg[r.name];
@@ -2019,11 +2019,11 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
   float* C = nullptr;
   const bool persistent = variant < 100;
   variant %= 100;
-  ZV_CHECK(hipMalloc(&A, (size_t)M * Kp * 2));
-  ZV_CHECK(hipMalloc(&W, (size_t)Np * Kp * 2));
-  if (out_mode != 0) ZV_CHECK(hipMalloc(&Ch, (size_t)M * N * 2));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&A, (size_t)M * Kp * 2)));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&W, (size_t)Np * Kp * 2)));
+  if (out_mode != 0) ZV_CHECK(ZV_BLOCKING(hipMalloc(&Ch, (size_t)M * N * 2)));
   if (out_mode == 0 || out_mode == 2) {
-    ZV_CHECK(hipMalloc(&C, (size_t)M * N * 4));
+    ZV_CHECK(ZV_BLOCKING(hipMalloc(&C, (size_t)M * N * 4)));
     ZV_CHECK(hipMemsetAsync(C, 0, (size_t)M * N * 4, s));
   }
   hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(4096), dim3(256), 0, s, A, (long)M * Kp, 1u);
@@ -2037,14 +2037,14 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
   if (out_mode == 4) { p.C = nullptr; p.Ch = nullptr; }
   float* extra = nullptr;          // modes 5 / 6: a residual linear's epilogue operands
   if (out_mode == 7) {             // a plain linear's: bias + SwooshL -> bf16 copy
-    ZV_CHECK(hipMalloc(&extra, (size_t)N * 4));
+    ZV_CHECK(ZV_BLOCKING(hipMalloc(&extra, (size_t)N * 4)));
     ZV_CHECK(hipMemsetAsync(extra, 0, (size_t)N * 4, s));
     p.C = nullptr; p.bias = extra; p.act = 1;
   }
   if (out_mode == 5 || out_mode == 6) {
-    ZV_CHECK(hipMalloc(&C, (size_t)M * N * 4));
+    ZV_CHECK(ZV_BLOCKING(hipMalloc(&C, (size_t)M * N * 4)));
     ZV_CHECK(hipMemsetAsync(C, 0, (size_t)M * N * 4, s));
-    ZV_CHECK(hipMalloc(&extra, (size_t)(2 * N + (out_mode == 6 ? (size_t)M * N : 0)) * 4));
+    ZV_CHECK(ZV_BLOCKING(hipMalloc(&extra, (size_t)(2 * N + (out_mode == 6 ? (size_t)M * N : 0)) * 4)));
     ZV_CHECK(hipMemsetAsync(extra, 0, (size_t)(2 * N + (out_mode == 6 ? (size_t)M * N : 0)) * 4, s));
     p.C = C; p.resid = C; p.bias = extra;
     if (out_mode == 6) { p.byp = extra + N; p.orig = extra + 2 * N; }
@@ -2087,25 +2087,25 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
     case 60: {                     // dual-group residual kernel (out mode 2 only)
       if (out_mode != 2) throw std::invalid_argument("variant 60: residual mode only");
       hipEvent_t e0, e1;
-      ZV_CHECK(hipEventCreate(&e0)); ZV_CHECK(hipEventCreate(&e1));
+      ZV_CHECK(ZV_BLOCKING(hipEventCreate(&e0))); ZV_CHECK(ZV_BLOCKING(hipEventCreate(&e1)));
       launch_gemm_dual(p, s, "bench");
       ZV_CHECK(hipEventRecord(e0, s));
       for (int i = 0; i < iters; ++i) launch_gemm_dual(p, s, "bench");
       ZV_CHECK(hipEventRecord(e1, s));
-      ZV_CHECK(hipEventSynchronize(e1));
+      ZV_CHECK(ZV_BLOCKING(hipEventSynchronize(e1)));
       ZV_CHECK(hipEventElapsedTime(&ms, e0, e1));
       ms /= iters;
-      ZV_CHECK(hipEventDestroy(e0)); ZV_CHECK(hipEventDestroy(e1));
+      ZV_CHECK(ZV_BLOCKING(hipEventDestroy(e0))); ZV_CHECK(ZV_BLOCKING(hipEventDestroy(e1)));
       break;
     }
 #endif
     default: throw std::invalid_argument("unknown variant");
   }
   *ms_out = ms;
-  ZV_CHECK(hipFree(A)); ZV_CHECK(hipFree(W));
-  if (extra) ZV_CHECK(hipFree(extra));
-  if (C) ZV_CHECK(hipFree(C));
-  if (Ch) ZV_CHECK(hipFree(Ch));
+  ZV_CHECK(ZV_BLOCKING(hipFree(A))); ZV_CHECK(ZV_BLOCKING(hipFree(W)));
+  if (extra) ZV_CHECK(ZV_BLOCKING(hipFree(extra)));
+  if (C) ZV_CHECK(ZV_BLOCKING(hipFree(C)));
+  if (Ch) ZV_CHECK(ZV_BLOCKING(hipFree(Ch)));
   ZV_API_END
 }
 
@@ -2166,18 +2166,18 @@ int zv_mx8_gemm_check(int M, int N, int K, const float* A, const float* W, float
   std::vector<uint8_t> wq((size_t)Np * K), ws((size_t)Np * K / MX8_BLOCK);
   mx8_quantize_host(wp.data(), K, (int)Np, K, wq.data(), K, ws.data());
   bf16* dA; uint8_t *dAq, *dAs, *dWq, *dWs; float *dC, *dB;
-  ZV_CHECK(hipMalloc(&dA, ah.size() * 2));
-  ZV_CHECK(hipMalloc(&dAq, (size_t)M * K));
-  ZV_CHECK(hipMalloc(&dAs, (size_t)M * K / MX8_BLOCK));
-  ZV_CHECK(hipMalloc(&dWq, wq.size()));
-  ZV_CHECK(hipMalloc(&dWs, ws.size()));
-  ZV_CHECK(hipMalloc(&dC, (size_t)M * N * 4));
-  ZV_CHECK(hipMalloc(&dB, (size_t)N * 4));
-  ZV_CHECK(hipMemcpy(dA, ah.data(), ah.size() * 2, hipMemcpyHostToDevice));
-  ZV_CHECK(hipMemcpy(dWq, wq.data(), wq.size(), hipMemcpyHostToDevice));
-  ZV_CHECK(hipMemcpy(dWs, ws.data(), ws.size(), hipMemcpyHostToDevice));
-  ZV_CHECK(hipMemset(dC, 0, (size_t)M * N * 4));
-  ZV_CHECK(hipMemset(dB, 0, (size_t)N * 4));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&dA, ah.size() * 2)));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&dAq, (size_t)M * K)));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&dAs, (size_t)M * K / MX8_BLOCK)));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&dWq, wq.size())));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&dWs, ws.size())));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&dC, (size_t)M * N * 4)));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&dB, (size_t)N * 4)));
+  ZV_CHECK(ZV_BLOCKING(hipMemcpy(dA, ah.data(), ah.size() * 2, hipMemcpyHostToDevice)));
+  ZV_CHECK(ZV_BLOCKING(hipMemcpy(dWq, wq.data(), wq.size(), hipMemcpyHostToDevice)));
+  ZV_CHECK(ZV_BLOCKING(hipMemcpy(dWs, ws.data(), ws.size(), hipMemcpyHostToDevice)));
+  ZV_CHECK(ZV_BLOCKING(hipMemset(dC, 0, (size_t)M * N * 4)));
+  ZV_CHECK(ZV_BLOCKING(hipMemset(dB, 0, (size_t)N * 4)));
   hipLaunchKernelGGL(zv_mx8_pack_kernel, grid1d((long)M * (K / 8)), dim3(256), 0, s, dA, (long)K, (long)M,
                      K, dAq, (long)K, dAs);
   ZV_LAUNCH_CHECK();
@@ -2187,12 +2187,12 @@ int zv_mx8_gemm_check(int M, int N, int K, const float* A, const float* W, float
   p.Bh = reinterpret_cast<const bf16*>(dWq); p.ldb = K; p.Bs = dWs; p.ldbs = K / MX8_BLOCK;
   p.bias = dB; p.C = dC; p.ldc = N; p.resid = dC; p.rows_per_group = 1; p.rpb = 1;
   launch_gemm<128, 128, 2, 2, 8, EPI_STD, 2, 2, MX8_KSTEP, 0, 0, 0, 1>(p, 1, s, "mx8_check", true, -1);
-  ZV_CHECK(hipDeviceSynchronize());
-  ZV_CHECK(hipMemcpy(C, dC, (size_t)M * N * 4, hipMemcpyDeviceToHost));
-  if (Aq) ZV_CHECK(hipMemcpy(Aq, dAq, (size_t)M * K, hipMemcpyDeviceToHost));
-  if (As) ZV_CHECK(hipMemcpy(As, dAs, (size_t)M * K / MX8_BLOCK, hipMemcpyDeviceToHost));
+  ZV_CHECK(ZV_BLOCKING(hipDeviceSynchronize()));
+  ZV_CHECK(ZV_BLOCKING(hipMemcpy(C, dC, (size_t)M * N * 4, hipMemcpyDeviceToHost)));
+  if (Aq) ZV_CHECK(ZV_BLOCKING(hipMemcpy(Aq, dAq, (size_t)M * K, hipMemcpyDeviceToHost)));
+  if (As) ZV_CHECK(ZV_BLOCKING(hipMemcpy(As, dAs, (size_t)M * K / MX8_BLOCK, hipMemcpyDeviceToHost)));
   for (void* ptr : {(void*)dA, (void*)dAq, (void*)dAs, (void*)dWq, (void*)dWs, (void*)dC, (void*)dB})
-    ZV_CHECK(hipFree(ptr));
+    ZV_CHECK(ZV_BLOCKING(hipFree(ptr)));
   ZV_API_END
 }
 
@@ -2202,12 +2202,12 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
   const long Kp = round_up(K, 64), Np = round_up(N, 256);
   bf16 *A, *W;
   float *C0, *C1, *R, *res;
-  ZV_CHECK(hipMalloc(&A, (size_t)M * Kp * 2));
-  ZV_CHECK(hipMalloc(&W, (size_t)Np * Kp * 2));
-  ZV_CHECK(hipMalloc(&C0, (size_t)M * N * 4));
-  ZV_CHECK(hipMalloc(&C1, (size_t)M * N * 4));
-  ZV_CHECK(hipMalloc(&R, (size_t)M * N * 4));
-  ZV_CHECK(hipMalloc(&res, 8));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&A, (size_t)M * Kp * 2)));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&W, (size_t)Np * Kp * 2)));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&C0, (size_t)M * N * 4)));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&C1, (size_t)M * N * 4)));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&R, (size_t)M * N * 4)));
+  ZV_CHECK(ZV_BLOCKING(hipMalloc(&res, 8)));
   hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(4096), dim3(256), 0, s, A, (long)M * Kp, 1u);
   hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(4096), dim3(256), 0, s, W, (long)Np * Kp, 2u);
   hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(4096), dim3(256), 0, s, reinterpret_cast<bf16*>(R),
@@ -2223,14 +2223,14 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
   float* outs[2] = {C0, C1};
   float* extra = nullptr;          // dual-group variants: bias, bypass original / scale
   if (variant == 72) {             // counted plain epilogue: bias (+ SwooshL) -> bf16
-    ZV_CHECK(hipMalloc(&extra, (size_t)N * 4));
+    ZV_CHECK(ZV_BLOCKING(hipMalloc(&extra, (size_t)N * 4)));
     hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(64), dim3(256), 0, s, reinterpret_cast<bf16*>(extra),
                        (long)N * 2, 5u);
     p.bias = extra;
   }
   if (variant == 60 || variant == 61 || variant == 70 || variant == 71) {
     if (mode != 2) throw std::invalid_argument("selftest: residual-only variant");
-    ZV_CHECK(hipMalloc(&extra, (size_t)(2 * N + (size_t)M * N) * 4));
+    ZV_CHECK(ZV_BLOCKING(hipMalloc(&extra, (size_t)(2 * N + (size_t)M * N) * 4)));
     hipLaunchKernelGGL(zv_fill_rand_bf16, dim3(4096), dim3(256), 0, s, reinterpret_cast<bf16*>(extra),
                        (long)(2 * N + (long)M * N) * 2, 4u);
     p.bias = extra;
@@ -2273,12 +2273,14 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
   ZV_CHECK(hipMemsetAsync(res, 0, 8, s));
   hipLaunchKernelGGL(zv_maxdiff_kernel, dim3(1024), dim3(256), 0, s, C1, C0, (long)M * N, res);
   float h[2];
-  ZV_CHECK(hipMemcpy(h, res, 8, hipMemcpyDeviceToHost));
+  ZV_CHECK(ZV_BLOCKING(hipMemcpy(h, res, 8, hipMemcpyDeviceToHost)));
   *maxdiff = h[0]; *maxref = h[1];
-  for (void* q : {(void*)A, (void*)W, (void*)C0, (void*)C1, (void*)R, (void*)res}) ZV_CHECK(hipFree(q));
-  if (extra) ZV_CHECK(hipFree(extra));
+  for (void* q : {(void*)A, (void*)W, (void*)C0, (void*)C1, (void*)R, (void*)res}) ZV_CHECK(ZV_BLOCKING(hipFree(q)));
+  if (extra) ZV_CHECK(ZV_BLOCKING(hipFree(extra)));
   ZV_API_END
 }
+
+int64_t zv_host_block_count(void) { return (int64_t)g_zv_host_blocks.load(); }
 
 int64_t zv_device_bytes(zv_handle h) {
   if (!h) return 0;
@@ -2316,8 +2318,8 @@ int zv_velocity(zv_handle h, float t, float guidance_scale, const float* x, cons
 // reference evaluates the same predicate on the host every step, solver.py:71)
 static bool any_nonzero_rows(const float* grows, int B, hipStream_t s) {
   std::vector<float> h(B);
-  ZV_CHECK(hipMemcpyAsync(h.data(), grows, (size_t)B * 4, hipMemcpyDeviceToHost, s));
-  ZV_CHECK(hipStreamSynchronize(s));
+  ZV_CHECK(ZV_BLOCKING(hipMemcpyAsync(h.data(), grows, (size_t)B * 4, hipMemcpyDeviceToHost, s)));
+  ZV_CHECK(ZV_BLOCKING(hipStreamSynchronize(s)));
   for (float v : h) if (v != 0.0f) return true;
   return false;
 }

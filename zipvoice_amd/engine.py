@@ -73,6 +73,7 @@ SIGNATURES = {
     "zv_bench_gemm": (_I, [_I, _I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_float)]),
     "zv_gemm_selftest": (_I, [_I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "zv_profile_report": (_I, [ctypes.c_char_p, _I]),
+    "zv_host_block_count": (ctypes.c_int64, []),
     "zv_attn_plan": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "zv_mx8_quantize": (_I, [_P, _I, _I, _P, _P]),
     "zv_mx8_gemm_check": (_I, [_I, _I, _I, _P, _P, _P, _P, _P]),
@@ -173,6 +174,13 @@ def profile(enable: bool, detail: bool = False):
     load_library()
     for lib in list(_libs.values()):
         _check(lib.zv_profile((2 if detail else 1) if enable else 0), lib)
+
+
+def host_block_count() -> int:
+    """Host-blocking HIP runtime calls issued so far, summed over the loaded engine libraries
+    (zv_host_block_count: allocations, synchronous copies, synchronisations, ...)."""
+    load_library()
+    return sum(int(lib.zv_host_block_count()) for lib in list(_libs.values()))
 
 
 def profile_report() -> dict:
