@@ -1746,9 +1746,13 @@ struct zv_engine {
     GraphKey key{B, T, num_step, pad ? 1 : 0, grows ? 0.f : g, t0, t1, shift,
                  grows ? (cfg_rows ? 1 : 2) : 0, g_ws_generation};
     auto it = graphs.find(key);
-    if (it == graphs.end() && graph_seen[key] == 0) {
-      if (graph_seen.size() > MAX_SEEN) { graph_seen.clear(); graph_seen[key] = 0; }
-      graph_seen[key] = 1;                       // warm-up: sizes the workspace
+    // seen-once shapes are keyed without the workspace generation: the warm-up run itself grows
+    // the workspace, and the next call of the shape should capture, not warm up again
+    GraphKey seen_key = key;
+    seen_key.gen = 0;
+    if (it == graphs.end() && graph_seen[seen_key] == 0) {
+      if (graph_seen.size() > MAX_SEEN) { graph_seen.clear(); graph_seen[seen_key] = 0; }
+      graph_seen[seen_key] = 1;                  // warm-up: sizes the workspace
       euler_loop(x, tc, sc, pad, B, T, ts, g, grows, cfg_rows, s);
       return;
     }
