@@ -89,7 +89,7 @@ int main(int argc, char** argv) {
   ZV_CHECK(hipMemset(flag, 0, 4096));
   ZV_CHECK(hipMemset(err, 0, 16));
   unsigned long long* dbg;
-  ZV_CHECK(hipMalloc(&dbg, 1024 * 4 * 6 * 8));
+  ZV_CHECK(hipMalloc(&dbg, 1024 * 4 * FFN_DBG_WORDS * 8));
   for (auto& sh : shapes) {
     const int M = sh[0], H = sh[1];
     const long Hp = round_up(H, 256);
@@ -247,15 +247,20 @@ int main(int argc, char** argv) {
       // the last launch's per-wave clock totals (FFN_TIMING build): where a chunk step goes
       {
         const int nb = ffn_schedule(cdiv(M, FFN_BM), H / FFN_HC, blocks_max > 0 ? blocks_max : zv_num_cus(), true).blocks;
-        std::vector<unsigned long long> hd((size_t)nb * 4 * 6);
+        const int W = FFN_DBG_WORDS;
+        std::vector<unsigned long long> hd((size_t)nb * 4 * W);
         ZV_CHECK(hipMemcpy(hd.data(), dbg, hd.size() * 8, hipMemcpyDeviceToHost));
-        double tot = 0, rt = 0, vm = 0, bar = 0, st = 0;
+        double tot = 0, rt = 0, vm = 0, bar = 0, st = 0, epi = 0, xw = 0, it = 0, lp = 0;
         for (int b = 0; b < nb * 4; ++b) {
-          tot += hd[b * 6]; rt += hd[b * 6 + 1]; vm += hd[b * 6 + 2]; bar += hd[b * 6 + 3]; st += hd[b * 6 + 4];
+          const unsigned long long* d = &hd[(size_t)b * W];
+          tot += d[0]; rt += d[1]; vm += d[2]; bar += d[3]; st += d[4]; epi += d[6]; xw += d[7]; it += d[8]; lp += d[9];
         }
+        const double nw = nb * 4.0;
         printf("    timing (last launch, per wave): %.0f clk total, %.1f us (%.2f GHz), %.0f steps, per step %.0f clk, "
-               "vmcnt wait %.0f, barrier %.0f\n", tot / (nb * 4), rt / (nb * 4) / 100.0, tot / rt * 0.1,
-               st / (nb * 4), tot / st, vm / st, bar / st);
+               "vmcnt wait %.0f, barrier %.0f\n", tot / nw, rt / nw / 100.0, tot / rt * 0.1, st / nw, tot / st, vm / st, bar / st);
+        printf("      %.1f items: epilogue %.0f clk/item (%.0f%%), item start (x landed) %.0f clk/item (%.0f%%), steady loop %.0f%%, "
+               "rest %.0f%%\n", it / nw, epi / it, 100 * epi / tot, xw / it, 100 * xw / tot, 100 * lp / tot,
+               100 * (tot - epi - xw - lp) / tot);
       }
 #endif
       fflush(stdout);

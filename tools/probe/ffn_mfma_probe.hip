@@ -11,7 +11,10 @@
 //   V5  V4 with the pieces spread one per 3 slots (slots 0, 3, ..., 45)
 //   V6  V2 + vmcnt(0) + barrier per step, no DMA
 //   V7  V2 + 2 independent v_fma_f32 per slot (VALU fillers)
-//   V8  V2 + 1 ds_read_b128 per slot (fragment re-reads, conflict-free)
+//   V8  V2 + 1 ds_read_b128 per slot, read into the consumed fragment's register 4 MFMAs of its
+//       kind ahead of use (the kernel's fragment ring)
+//   V9  V4 + V8 + the activation's micro-op pattern (per 4 slots: add+fmamk, min+exp, add+log,
+//       fmamk+max+fmamk on a dependent chain) + the per-step barrier: the whole chunk step's skeleton
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probe/ffn_mfma_probe.hip -o tools/probe/ffn_mfma_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -65,6 +68,7 @@ __global__ __launch_bounds__(256, 1) void probe(const __bf16* src, const void* w
     const unsigned ldsb = (unsigned)(uintptr_t)smem + (st & 1) * 65536 + wave * 16384;
     sfor<64>([&](auto K_) {
       constexpr int k = decltype(K_)::value, i = k >> 1;
+      float& g0 = f0; float& g1 = f1; float& g2 = f2; float& g3 = f3;   // (captured in every instantiation)
       if constexpr ((k & 1) == 0) {
         if constexpr (V != 1) {
           if constexpr (V == 3) mma_a(h, fa[i & 3], xf[i]);
@@ -73,7 +77,19 @@ __global__ __launch_bounds__(256, 1) void probe(const __bf16* src, const void* w
       } else {
         if constexpr (V != 0) mma_a(out[i >> 1], fb[i & 3], hb[i & 1]);
       }
-      if constexpr (V == 4) {
+      if constexpr (V == 8 || V == 9) {
+        // after MFMA i of its kind: its fragment register gets the one for MFMA i + 4
+        if constexpr ((k & 1) == 0) fa[i & 3] = *reinterpret_cast<const bf16x8*>(smem + 131072 + ((i + 4) & 7) * 1024 + lfr);
+        else fb[i & 3] = *reinterpret_cast<const bf16x8*>(smem + 139264 + ((i + 4) & 7) * 1024 + lfr);
+      }
+      if constexpr (V == 9) {
+        constexpr int sub = k & 3;
+        if constexpr (sub == 0) asm volatile("v_add_f32 %0, %0, %1\n\tv_fmamk_f32 %1, %0, 0x3fb8aa3b, %2" : "+v"(g0), "+v"(g1) : "v"(g3));
+        if constexpr (sub == 1) asm volatile("v_min_f32 %0, 0x42fc0000, %1\n\tv_exp_f32 %0, %0" : "=v"(g2) : "v"(g1));
+        if constexpr (sub == 2) asm volatile("v_add_f32 %0, 1.0, %0\n\tv_log_f32 %0, %0" : "+v"(g2));
+        if constexpr (sub == 3) asm volatile("v_fmamk_f32 %0, %1, 0xbda3d70a, %2\n\tv_max_f32 %1, %1, %2\n\tv_fmamk_f32 %0, %1, 0x3f317218, %0" : "+v"(g3), "+v"(g2) : "v"(g1));
+      }
+      if constexpr (V == 4 || V == 9) {
         if constexpr (k == 1 || k == 17 || k == 33 || k == 49) {
           const int b = (k - 1) / 16;
 #pragma unroll
@@ -91,14 +107,10 @@ __global__ __launch_bounds__(256, 1) void probe(const __bf16* src, const void* w
         }
       }
       if constexpr (V == 7) {
-        asm volatile("v_fma_f32 %0, %0, %1, %1\n\tv_fma_f32 %2, %2, %3, %3" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
-      }
-      if constexpr (V == 8) {
-        bf16x8 r = *reinterpret_cast<const bf16x8*>(smem + 131072 + (k & 7) * 1024 + lfr);
-        asm volatile("" :: "v"(r));
+        asm volatile("v_fma_f32 %0, %0, %1, %1\n\tv_fma_f32 %2, %2, %3, %3" : "+v"(g0), "+v"(g1), "+v"(g2), "+v"(g3));
       }
     });
-    if constexpr (V == 4 || V == 5 || V == 6) {
+    if constexpr (V == 4 || V == 5 || V == 6 || V == 9) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
@@ -146,6 +158,7 @@ int main(int argc, char** argv) {
   run<6>(src, w, sink, cyc, steps, blocks);
   run<7>(src, w, sink, cyc, steps, blocks);
   run<8>(src, w, sink, cyc, steps, blocks);
+  run<9>(src, w, sink, cyc, steps, blocks);
   printf("(constant operands: compare variants; s_memtime counts shader cycles)\n");
   return 0;
 }
