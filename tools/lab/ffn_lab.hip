@@ -152,7 +152,7 @@ int main(int argc, char** argv) {
           if (norm) {
             // FF3 + BiasNorm: resid = the working stream (C0 copy in Co), orig = C (in place)
             g.resid = orig + (long)r0 * D; g.orig = Co + (long)r0 * D; g.C = Co + (long)r0 * D;
-            g.Cl = Clo + (long)r0 * D; g.C2h = C2ho + (long)r0 * D;
+            g.C2h = C2ho + (long)r0 * D;   // the engine's 16-bit set: the next layer's copy (no Cl)
             g.rowvec = rowvec; f.rowvec_ld = 0; f.rows_per_group = 1219;
             f.byp = byp; f.nb = nb; f.log_scale = 0.3f;
           }
