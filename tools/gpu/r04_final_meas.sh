@@ -23,7 +23,6 @@ for kv in "r04_gemm_resid_r1:zv_gemm_kernel<128, 128, 2, 2, 1, 0, 2, 2, 64, 0, 0
 done
 cut -c1-220 $O/pmc_traffic.log
 rm -f $F $W
-mkdir -p profiles_new && cp $O/r04_*_traffic.json profiles_new/ && cp profiles_new/r04_*_traffic.json profiles/
 step bench
 timeout -k 10 500 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/bench.json'));print(d['ms_per_step'],d['value'],d['roofline']['kernel'],d['roofline']['frac'],d['roofline'].get('traffic_over_algorithmic'));print({k:v['ms_per_step'] for k,v in d.items() if isinstance(v,dict) and 'ms_per_step' in v})"
