@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round 4 GPU session I: the transposed FF epilogue with its per-pass constants loaded ahead of the
+# prefetch stream (no drain per pass) vs the per-lane one, lab + phase timing; the FF / split / parity
+# tests; bench A/B against an FFN_EPI_T=0 engine (ab_libs/, python zipvoice_amd/csrc/build.py
+# --out ab_libs/libzipvoice_hip_noT.so -DFFN_EPI_T=0).
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r04_i}; mkdir -p $O
+for r in 1 2; do
+  for v in ffn_lab_noT ffn_lab; do
+    echo "== $v round $r" >> $O/var.txt
+    timeout -k 10 120 tools/lab/$v 3 1,2,4 "78016x1536;26005x1536" 0 "classic,pers" >> $O/var.txt 2>&1 || { echo "$v rc=$?"; tail -5 $O/var.txt; exit 1; }
+  done
+done
+cat $O/var.txt
+for v in t t_noT; do
+  echo "== $v" >> $O/x.txt
+  timeout -k 10 60 tools/lab/ffn_lab_$v 2 1,2,4 "78016x1536" 0 "pers" >> $O/x.txt 2>&1 || { echo "$v rc=$?"; tail -3 $O/x.txt; exit 1; }
+done
+cat $O/x.txt
+timeout -k 10 900 python -u -m pytest tests/test_gpu_ffn.py tests/test_gpu_split_streams.py tests/test_gpu_parity.py "tests/test_gpu_fullsize.py::test_velocity_full_size_fp16_fused_ff" "tests/test_gpu_fullsize.py::test_c2_batch_rows_equal_single_utterance" -x -q --timeout 400 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed"; grep -E "FAIL|Error|error" $O/pytest.log | tail -30; exit 1; }
+tail -2 $O/pytest.log
+bash tools/gpu/ab_env.sh ${1:-r04_i}/ab 2 "-" "ZV_LIB_PATH=ab_libs/libzipvoice_hip_noT.so"
