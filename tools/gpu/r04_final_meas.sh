@@ -14,8 +14,8 @@ F=$(ls $O/pmc_fetch/*counter_collection.csv | head -1); W=$(ls $O/pmc_write/*cou
 for kv in "r04_gemm_resid_r1:zv_gemm_kernel<128, 128, 2, 2, 1, 0, 2, 2, 64, 0, 0, 0, 1, 1, 0>" \
           "r04_gemm_resid_r4:zv_gemm_kernel<128, 128, 2, 2, 1, 0, 2, 2, 64, 0, 0, 0, 4, 1, 0>" \
           "r04_gemm_resid_r2:zv_gemm_kernel<128, 128, 2, 2, 1, 0, 2, 2, 64, 0, 0, 0, 2, 1, 0>" \
-          "r04_ffn:zv_ffn_kernel<(true|false), (true|false), true, 0, 0>" \
-          "r04_ffn_norm:zv_ffn_kernel<false, false, true, 0, 1>" \
+          "r04_ffn:zv_ffn_kernel<(true|false), (true|false), true, 0, 0, (true|false)>" \
+          "r04_ffn_norm:zv_ffn_kernel<false, false, true, 0, 1, true>" \
           "r04_ffn_all:zv_ffn_kernel<" \
           "r04_gemm:zv_gemm_kernel<128, 128, 2, 2, 1, 0, 2, 2, 64, 0, 0, 0, 3, 1, 0>"; do
   n=${kv%%:*}; rx=${kv#*:}
