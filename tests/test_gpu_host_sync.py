@@ -9,6 +9,7 @@ split decoder streams, the prompt split and the Vocos vocoder) at an already-see
     (torch.cuda.set_sync_debug_mode("error") raises on one).  The only host read of the step is
     the output lengths, taken before sampling (models.py: sample), where the text path has
     already synchronised for num_frames."""
+import gc
 import os
 import sys
 
@@ -64,9 +65,17 @@ def test_warm_step_has_no_host_block(monkeypatch, split):
 
     monkeypatch.setattr(model.solver, "sample", guarded_sample)
     monkeypatch.setattr(voc, "decode_features", guarded_decode)
-    c0 = engine.host_block_count()
-    wav, lens = job.compute(shard)
-    c1 = engine.host_block_count()
+    # engines of earlier tests that the garbage collector finalises inside the measured step would
+    # count their own frees: collect them first and keep the collector out of the step
+    gc.collect()
+    torch.cuda.synchronize()
+    gc.disable()
+    try:
+        c0 = engine.host_block_count()
+        wav, lens = job.compute(shard)
+        c1 = engine.host_block_count()
+    finally:
+        gc.enable()
     torch.cuda.synchronize()
     print(f"split={split}: host-blocking engine calls in a warm step {c1 - c0} "
           f"(solver entry -> vocoder return {inner['c1'] - inner['c0']}); torch sync guard "
