@@ -213,11 +213,14 @@ def _kernel_roofline(name, r, total_ms):
 
 
 def roofline(job):
-    """One extra, untimed step with the engine's per-launch HIP-event profiler on, on the
-    timed schedule (the decoder's three row-block streams: the launch set the rocprofv3
-    summary of the bench command and the PMC traffic files also see): the dominant kernel's
-    algorithmic work per launch / its average duration (HIP events on the launch stream), and
-    the residual-linear family (the HBM-bound one) per epilogue ROLE as `secondary`."""
+    """One extra, untimed step with the engine's per-launch HIP-event profiler on: the timed
+    step's launches (the decoder's three row blocks, the same kernels and shapes: the launch set
+    the rocprofv3 summary of the bench command and the PMC traffic files also see), run one row
+    block after another so that each event pair times its launch alone (overlapping on three
+    streams, an event pair also timed the co-running kernels; rocprofv3's kernel trace serialises
+    the dispatches the same way).  The dominant kernel's algorithmic work per launch / its
+    average duration, and the residual-linear family (the HBM-bound one) per epilogue ROLE as
+    `secondary`."""
     from zipvoice_amd import engine
     torch.cuda.synchronize()
     engine.profile(True)

@@ -1591,8 +1591,10 @@ struct zv_engine {
     if (stereo()) sidx = (Fin == dec.in_proj[0].K) ? 0 : 1;
     ZV_REQUIRE(Fin == dec.in_proj[sidx].K, "decoder input width does not match in_proj");
     io_split = cfg.precision == ZV_MIXED;
-    // (profiled passes run the same schedule as the timed ones: their per-launch event durations,
-    // the rocprofv3 trace of the bench command and the PMC traffic files describe one launch set)
+    // (profiled passes run the same launches as the timed ones -- the same row blocks, kernels and
+    // shapes -- but one row block after another on the caller's stream, so each launch's events time
+    // it alone: with the blocks overlapping on three streams an event pair timed the co-running
+    // kernels as well; rocprofv3's kernel trace serialises the dispatches the same way)
     if (split_streams < 2 || N < 2 || (long)N * T < split_min_rows) {
       decoder_rows(ws_dec, xin, sidx, N, T, pad, t, g, out, s);
       return;
@@ -1616,7 +1618,7 @@ struct zv_engine {
     // the joined FeedForward (ffn_site) needs the row blocks' host code interleaved: coroutines
     // on this thread (also under stream capture: the joins are event dependencies of the graph,
     // and the warm-up run that sizes the workspace took the same path)
-    const bool join = ffn_join && ffn_fused;
+    const bool join = ffn_join && ffn_fused && !g_zv_prof.on;
     std::vector<std::function<void()>> fns;
     int r0 = 0;
     for (int i = 0; i < parts; ++i) {
@@ -1625,8 +1627,9 @@ struct zv_engine {
       Act xi = xin;
       xi.h += rows * xin.ld;
       if (xin.l) xi.l += rows * xin.ld;
-      hipStream_t si = i == 0 ? s : split_stream[i - 1];
-      if (i > 0) ZV_CHECK(hipStreamWaitEvent(si, split_fork, 0));
+      const bool serial = g_zv_prof.on;
+      hipStream_t si = (i == 0 || serial) ? s : split_stream[i - 1];
+      if (i > 0 && !serial) ZV_CHECK(hipStreamWaitEvent(si, split_fork, 0));
       Workspace* wsi = i == 0 ? &ws_dec : &ws_split[i - 1];
       const uint8_t* padi = pad ? pad + rows : nullptr;
       const float* ti = t + r0;
@@ -1649,7 +1652,7 @@ struct zv_engine {
     }
     dec_rows_N = 0;
     dec_parts = 0;
-    for (int i = 1; i < parts; ++i) {
+    for (int i = 1; i < parts && !g_zv_prof.on; ++i) {
       ZV_CHECK(hipEventRecord(split_join[i - 1], split_stream[i - 1]));
       ZV_CHECK(hipStreamWaitEvent(s, split_join[i - 1], 0));
     }
