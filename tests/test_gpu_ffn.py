@@ -89,3 +89,25 @@ def test_dwconv_pipe_bitwise(monkeypatch):
         outs.append(o)
     for o in outs[1:]:
         assert np.array_equal(o, outs[0]), np.abs(o - outs[0]).max()
+
+
+def test_fused_ffn_short_utterances(monkeypatch):
+    """Utterances shorter than a wave's 32 rows at the downsampled stacks (T = 40: 20 / 10 frames at
+    ds 2 / 4): the row-vector epilogues whose groups are shorter than a wave take their per-lane
+    forms (the transposed FF1 epilogue's TP = false instantiation, the FF3 + BiasNorm epilogue's
+    global row-vector loads instead of the staged LDS rows).  Fused vs the oracle at the bf16 bar and
+    vs the unfused pair."""
+    from oracle.zipvoice_np import ZipVoiceOracle
+    outs = {}
+    for ffn in ("0", "2"):
+        outs[ffn], inp = _run(monkeypatch, {"ZV_FFN": ffn, "ZV_FFN_MIN_ROWS": "0"}, "bf16", B=8, T=40,
+                              lens=(40, 33, 40, 17, 25, 40, 9, 31), t=0.6, seed=5)
+    cfg, sd, x, tc, sc, pm, t = inp
+    ref = ZipVoiceOracle(cfg, sd).velocity(np.float32(t), x, tc, sc, pm, 1.0)
+    valid = ~pm
+    for ffn, o in outs.items():
+        e = np.abs(o - ref)[valid]
+        print(f"short utterances ZV_FFN={ffn}: vs oracle mean {e.mean():.3e} max {e.max():.3e}; "
+              f"vs unfused {np.abs(o - outs['0'])[valid].mean():.3e}")
+        assert np.isfinite(o).all()
+        assert e.mean() < BAR["bf16"], (ffn, e.mean())
