@@ -203,7 +203,19 @@ static StreamSet acquire_stream_set() {
   }
   StreamSet set;
   set.dev = dev;
-  for (auto& st : set.s) ZV_CHECK(ZV_BLOCKING(hipStreamCreateWithFlags(&st, hipStreamNonBlocking)));
+  // ZV_STREAM_PRIO (scheduling experiment, default 0): the split decoder's row-block streams (slots
+  // 0 .. ZV_STREAM_SET - 2; row block 0 runs on the caller's stream) at the device's greatest (> 0)
+  // or least (< 0) priority, so the CUs a finished kernel frees go to one side's waiting blocks first
+  const char* pe = getenv("ZV_STREAM_PRIO");
+  const int prio_mode = pe ? atoi(pe) : 0;
+  int least = 0, greatest = 0;
+  if (prio_mode) ZV_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  for (int i = 0; i < ZV_STREAM_SET; ++i) {
+    if (prio_mode && i < ZV_STREAM_SET - 1)
+      ZV_CHECK(ZV_BLOCKING(hipStreamCreateWithPriority(&set.s[i], hipStreamNonBlocking, prio_mode > 0 ? greatest : least)));
+    else
+      ZV_CHECK(ZV_BLOCKING(hipStreamCreateWithFlags(&set.s[i], hipStreamNonBlocking)));
+  }
   return set;
 }
 static void release_stream_set(const StreamSet& set) {
@@ -413,7 +425,8 @@ struct zv_engine {
 
   // ---------------------------------------------------------------- joined FeedForward
   // ZV_FFN_PERSIST (default 1): fused FeedForward launches on the persistent line schedule
-  // (zv_ffn.inc; results equal to one row block per block bit for bit).  ZV_FFN_JOIN (default 1):
+  // (zv_ffn.inc; results equal to one row block per block bit for bit).  ZV_FFN_JOIN (default 0:
+  // its cross-stream events cost more than the fill gains, bench 458-464 vs 417 ms):
   // with the decoder's rows split over streams, the row blocks' FeedForward modules run as ONE
   // launch over all rows: the line schedule needs the whole batch (C2 per stream: 204 row blocks
   // for 256 CUs -- one round at best -- against 610 as one launch, 2.4 rounds of work in 2.42).
