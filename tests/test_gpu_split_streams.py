@@ -1,4 +1,4 @@
-"""Decoder row blocks on 2-4 streams (ZV_SPLIT_STREAMS, zv_engine::decoder; default 3)
+"""Decoder row blocks on 2-4 streams (ZV_SPLIT_STREAMS, zv_engine::decoder; default 4)
 against the single-stream decoder (ZV_SPLIT_STREAMS=1): rows never interact on the path
 (every kernel is per row, per (row, head) or per output element with a fixed K order), so
 the velocity, a guided Euler solve replayed from its graph, and the per-utterance-guidance
@@ -22,7 +22,8 @@ def _inputs(B, T, lens, seed):
 
 @pytest.mark.parametrize("variant,precision,parts", [("zipvoice", "bf16", "2"), ("zipvoice", "fp32", "2"),
                                                      ("zipvoice_distill", "bf16", "2"),
-                                                     ("zipvoice", "bf16", "3"), ("zipvoice", "fp16", "4")])
+                                                     ("zipvoice", "bf16", "3"), ("zipvoice", "bf16", "4"),
+                                                     ("zipvoice", "fp16", "4")])
 def test_split_streams_bitwise(monkeypatch, variant, precision, parts):
     from zipvoice_amd.config import default_config
     from zipvoice_amd.models import build_model
