@@ -21,7 +21,7 @@ torch = pytest.importorskip("torch")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-@pytest.mark.parametrize("split", ["4", "1"])
+@pytest.mark.parametrize("split", ["3", "1"])
 def test_warm_step_has_no_host_block(monkeypatch, split):
     import bench
     from zipvoice_amd import engine

@@ -1,4 +1,4 @@
-"""Decoder row blocks on 2-4 streams (ZV_SPLIT_STREAMS, zv_engine::decoder; default 4)
+"""Decoder row blocks on 2-4 streams (ZV_SPLIT_STREAMS, zv_engine::decoder; default 3)
 against the single-stream decoder (ZV_SPLIT_STREAMS=1): rows never interact on the path
 (every kernel is per row, per (row, head) or per output element with a fixed K order), so
 the velocity, a guided Euler solve replayed from its graph, and the per-utterance-guidance

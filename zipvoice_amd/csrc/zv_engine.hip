@@ -248,7 +248,7 @@ struct zv_engine {
   Workspace ws_dec, ws_txt;
   static constexpr int MAX_SPLIT = 4;
   Workspace ws_split[MAX_SPLIT - 1];   // row blocks 1.. of the split decoder
-  int split_streams = 4;           // ZV_SPLIT_STREAMS: decoder row blocks on this many streams
+  int split_streams = 3;           // ZV_SPLIT_STREAMS: decoder row blocks on this many streams
                                    // (<= 1: one stream; bench A/B: profiles/r02_split_tp_ab.txt)
   long split_min_rows = 0;         // ... for N*T >= this many rows (ZV_SPLIT_MIN_ROWS)
   hipStream_t split_stream[MAX_SPLIT - 1] = {};
@@ -368,7 +368,7 @@ struct zv_engine {
     ZV_REQUIRE(!gemm_pp && !gemm_dual && !resid_ws,
                "ZV_GEMM_PP / ZV_GEMM_DUAL / ZV_RESID_WS need the A/B build (build.py -DZV_AB_KERNELS)");
 #endif
-    split_streams = envi("ZV_SPLIT_STREAMS", 4);
+    split_streams = envi("ZV_SPLIT_STREAMS", 3);
     split_min_rows = envi("ZV_SPLIT_MIN_ROWS", 8192);
     gemm256 = envi("ZV_GEMM256", 2);
     gemm256_min_tiles = envi("ZV_GEMM256_MIN_TILES", 256);
