@@ -136,6 +136,8 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
  * the plain kernel, 0 / 1: the Toeplitz kernel without / with the table's lo half),
  * NonlinAttention of value width nv_na with scoring form tpm, the head-0 statistics — and
  * whether the fused path is taken (fits = 1) or the W-materialising fallback (0).
+ * tpm = 3: the second-generation set of the bf16 / fp8 engines (zv_flash2.inc: base-2 scores,
+ * no statistics pass, lds_stats = 0; sa_plo ignored).
  * split: 1 (16-bit operands) or 3 (fp32-accurate hi/lo). */
 int zv_attn_plan(int split, int sa_plo, int tpm, int L, int nv_na, int64_t* lds_sa, int64_t* lds_na,
                  int64_t* lds_stats, int* fits);

@@ -10,7 +10,8 @@ import pytest
 LIM = 160 * 1024
 # (split, sa_plo, tpm): the kernel sets zv_engine's layer() launches per mode
 MODES = {
-    "bf16/fp8": (1, 0, 1),        # Toeplitz SA, Toeplitz head-0 stats + NonlinAttention
+    "bf16/fp8": (1, 0, 3),        # second generation (zv_flash2.inc): base-2 scores, no stats pass
+    "bf16/fp8 ZV_ATTN2=0": (1, 0, 1),   # Toeplitz SA, Toeplitz head-0 stats + NonlinAttention
     "fp16 mixed": (1, 1, 0),      # Toeplitz SA with the table's lo half, fp32-table NA
     "16-bit no-tp": (1, -1, 0),   # ZV_SA_TP=0 A/B arm
     "fp32": (3, -1, 0),

@@ -82,12 +82,10 @@ int main(int argc, char** argv) {
   ZV_CHECK(hipEventCreate(&e0));
   ZV_CHECK(hipEventCreate(&e1));
   const int D = FFN_D;
-  float* part; unsigned *flag, *err;
+  float* part; unsigned* flag;
   ZV_CHECK(hipMalloc(&part, 512 * FFN_PART_FLOATS * 4));
   ZV_CHECK(hipMalloc(&flag, 4096));
-  ZV_CHECK(hipMalloc(&err, 16));
   ZV_CHECK(hipMemset(flag, 0, 4096));
-  ZV_CHECK(hipMemset(err, 0, 16));
   unsigned long long* dbg;
   ZV_CHECK(hipMalloc(&dbg, 1024 * 4 * FFN_DBG_WORDS * 8));
   for (auto& sh : shapes) {
@@ -138,7 +136,7 @@ int main(int argc, char** argv) {
         FfnParams f{};
         f.H = H; f.nseg = nseg; f.ldx = D; f.ldc = D; f.ldch = D; f.rows_per_group = 1;
         f.W1f = W1f; f.b1 = b1; f.W2f = W2f; f.b2 = b2;
-        if (pers) { f.part = part; f.flag = flag; f.err = err; }
+        if (pers) { f.part = part; f.flag = flag; f.part_slots = 512; }
         f.dbg = dbg;
         const int cut[4] = {0, M / 3 + 77, 2 * M / 3 + 5, M};
         for (int i = 0; i < nseg; ++i) {
@@ -203,9 +201,13 @@ int main(int argc, char** argv) {
       reset(C3); launch_ffn(f3, s, "lab", blocks_max);
       cmp(C3, C2, h);
       n16 = cmp16(Ch3, Ch2) + (norm ? cmp16(Cl3, Cl2) + cmp16(C2h3, C2h2) : 0);
-      unsigned herr = 0;
-      ZV_CHECK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
-      printf("  seg3!=classic %u+%u  err %u", ((unsigned*)h)[3], n16, herr);
+      // every hand-off flag must be back at zero between launches (a C item that did not reset
+      // its flag would let the next launch's C item skip its wait and read stale tiles)
+      std::vector<unsigned> hf(1024);
+      ZV_CHECK(hipMemcpy(hf.data(), flag, 4096, hipMemcpyDeviceToHost));
+      unsigned nflag = 0;
+      for (unsigned v : hf) nflag += v != 0;
+      printf("  seg3!=classic %u+%u  flags set %u", ((unsigned*)h)[3], n16, nflag);
       const int nc = H / FFN_HC;
       const FfnSchedule sc = ffn_schedule(cdiv(M, FFN_BM), nc, blocks_max > 0 ? blocks_max : zv_num_cus(), true);
       printf("  (R %d nc %d w %d blocks %d)\n", cdiv(M, FFN_BM), nc, sc.w, sc.blocks);

@@ -19,26 +19,15 @@
 #include <tuple>
 #include <vector>
 
-#include <ucontext.h>
 
 #include "zv_common.h"
 #include "zv_gemm.inc"
 #include "zv_gemm256.inc"
 #include "zv_ffn.inc"
-// Rejected GEMM designs kept as measured A/B arms: compiled only into an A/B
-// build (build.py --out PATH -DZV_AB_KERNELS); the product library carries default-path
-// kernels only, and the environment switches that select them throw without it.
-#ifdef ZV_AB_KERNELS
-#include "zv_gemm_ws.inc"
-#include "zv_gemm_dual.inc"
-#include "zv_gemm_pp.inc"
-#define ZV_AB_TAG " ab_kernels"
-#else
-#define ZV_AB_TAG ""
-#endif
 #include "zv_attn.inc"
 #include "zv_elem.inc"
 #include "zv_flash.inc"
+#include "zv_flash2.inc"
 #include "../../include/zipvoice_hip.h"
 
 static thread_local std::string g_last_error;
@@ -203,19 +192,10 @@ static StreamSet acquire_stream_set() {
   }
   StreamSet set;
   set.dev = dev;
-  // ZV_STREAM_PRIO (scheduling experiment, default 0): the split decoder's row-block streams (slots
-  // 0 .. ZV_STREAM_SET - 2; row block 0 runs on the caller's stream) at the device's greatest (> 0)
-  // or least (< 0) priority, so the CUs a finished kernel frees go to one side's waiting blocks first
-  const char* pe = getenv("ZV_STREAM_PRIO");
-  const int prio_mode = pe ? atoi(pe) : 0;
-  int least = 0, greatest = 0;
-  if (prio_mode) ZV_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-  for (int i = 0; i < ZV_STREAM_SET; ++i) {
-    if (prio_mode && i < ZV_STREAM_SET - 1)
-      ZV_CHECK(ZV_BLOCKING(hipStreamCreateWithPriority(&set.s[i], hipStreamNonBlocking, prio_mode > 0 ? greatest : least)));
-    else
-      ZV_CHECK(ZV_BLOCKING(hipStreamCreateWithFlags(&set.s[i], hipStreamNonBlocking)));
-  }
+  // (row-block streams at the greatest / least priority lost 1.9 % / 0.6 % per C2 step, round 4:
+  // profiles/r04_stream_prio.txt; all streams at the default priority)
+  for (int i = 0; i < ZV_STREAM_SET; ++i)
+    ZV_CHECK(ZV_BLOCKING(hipStreamCreateWithFlags(&set.s[i], hipStreamNonBlocking)));
   return set;
 }
 static void release_stream_set(const StreamSet& set) {
@@ -238,6 +218,7 @@ inline dim3 grid1d(long n, int block = 256) {
 struct zv_engine {
   zv_config cfg;
   std::map<std::string, std::vector<float>> staged;
+  std::map<std::string, std::vector<float>> derived;   // re-laid-out copies (stage_rows_scaled, ...)
   std::vector<void*> allocs;
   size_t weight_bytes = 0;
   bool ready = false;
@@ -255,23 +236,23 @@ struct zv_engine {
   hipEvent_t split_fork = nullptr, split_join[MAX_SPLIT - 1] = {};
 
   bool materialize_attn = false;   // A/B: ZV_ATTN_MATERIALIZE=1 keeps the W-materialising path
-  // GEMM launch policy by epilogue class: two 4-wave blocks per CU everywhere (OCC 2,
-  // profiles/r01_gemm_policy_ab.txt) and one tile per block (gridx -1): with the decoder
-  // split over streams, dynamically dispatched tiles fill the CUs another stream's kernel
-  // leaves idle; the persistent resident grid (0) measured 2.6 % slower for the plain and
-  // fused-epilogue linears (profiles/r02_launch_policy_ab.txt)
-  int occ_plain = 2, occ_resid = 2, occ_fused = 2;
-  int gridx_plain = -1, gridx_resid = -1, gridx_fused = -1;
-  int gemm_dual = 0;               // ZV_GEMM_DUAL: residual linears (K >= 64) on the dual-group
-                                   // kernel (zv_gemm_dual.inc); bitwise equal, A/B arm
-  int gemm_pp = 0;                 // ZV_GEMM_PP: bf16 linears with N % 128 == 0 (and the GLU / NA
-                                   // in-projections) on the ping-pong kernel (zv_gemm_pp.inc);
-                                   // 0 = the 128x128 kernels (A/B arm, bitwise equal)
-  int resid_ws = 0;                // residual linears on the wave-specialised epilogue kernel:
-                                   // ZV_RESID_WS 1 = K <= 64 only, 2 = all, 0 = none (default: since the
-                                   // counted epilogue, zv_gemm_kernel is faster there too - fp8-mode SA
-                                   // out-projections 50.0 -> 28.7 ms per step, profiles/r02_fp8_ws_ab.txt)
-  int n96_mode = 2;                // ZV_N96: the attention-score projection's tiles (see linear16)
+  // Measured launch-policy choices, fixed (their A/B knobs were retired in round 5; the records
+  // stay in profiles/): two 4-wave GEMM blocks per CU everywhere (profiles/r01_gemm_policy_ab.txt)
+  // and one tile per block (gridx -1: with the decoder split over streams, dynamically dispatched
+  // tiles fill the CUs another stream's kernel leaves idle; the persistent resident grid measured
+  // 2.6 % slower, profiles/r02_launch_policy_ab.txt); the attention-score projection on 128x128
+  // counted tiles (r02_n96_counted_ab.txt); the V^T projection on 64x64 tiles (r01_skinny_ab.txt);
+  // the copy-only SelfAttention out-projection on the counted epilogue (r02_sa_copy_ab.txt); no
+  // deferred stores (r01_gemm_defer_ab.txt); the 256x256 kernel from 256 tiles up.
+  static constexpr int occ_plain = 2, occ_resid = 2, occ_fused = 2;
+  static constexpr int gridx_plain = -1, gridx_resid = -1, gridx_fused = -1;
+  static constexpr int n96_mode = 2;
+  static constexpr bool sa_copy = true, skinny_tiles = true, defer_stores = false;
+  static constexpr int gemm256_min_tiles = 256;
+  // mixed (fp16 parity) mode: no lo half of the SelfAttention Toeplitz table, the fp32 positional
+  // table for the head-0 / NonlinAttention scoring, the weight-split attention-score projection
+  // (profiles/r03_mixed_ab.txt)
+  static constexpr bool mixed_plo = false, mixed_tpna = true, mixed_wsplit = true;
   // ZV_FFN: the decoder FeedForward modules as one fused kernel each (zv_ffn.inc: in_proj ->
   // SwooshL -> out_proj -> residual without the hidden tensor in HBM) for launches of at
   // least ffn_min_rows rows; 2 (default): FF3 also carries the layer's BiasNorm + bypass in its
@@ -287,96 +268,47 @@ struct zv_engine {
   // ZV_FFN_MIN_ROWS=0 pins the fused kernel for a batch-invariant engine
   // (tests/test_gpu_fullsize.py batch rows test)
   long ffn_min_rows = 10000;
-  bool ff1_src = true;             // ZV_FF1_SRC: FF1's residual read as src + temb (row vector) instead
-                                   // of a working stream BiasNorm / the stack entry wrote in fp32
-  bool sa_copy = true;             // ZV_SA_COPY: the copy-only SelfAttention out-projection on the
-                                   // counted epilogue (ROLE 5) instead of the wave-specialised kernel
-                                   // (bitwise equal; 36.3 -> 17.0 ms per step, profiles/r02_sa_copy_ab.txt)
-  bool kcat_sa = true;             // ZV_KCAT_SA (bf16 mode): SelfAttention out-projection's fp32
-                                   // update folded into the conv out-projection (K concatenation)
   int fp8_fuse = 7;                // ZV_FP8_FUSE (fp8 mode): which bf16 producers write the fp8 copy
-                                   // themselves (1 wave-specialised residual epilogue, 2 depthwise
-                                   // conv, 4 BiasNorm); the others are followed by the pack kernel
+                                   // themselves (2 depthwise conv, 4 BiasNorm; bit 1 is unused since
+                                   // the wave-specialised epilogue's removal); the others are followed
+                                   // by the pack kernel
   int sa_tp = 1;                   // ZV_SA_TP: 16-bit modes' SelfAttention with the positional
                                    // term on the MFMA chain (zv_attn_sa_tp_kernel), the head-0
                                    // stats / NonlinAttention scoring too; 0 = VALU forms
                                    // (3: A/B arm, SA with the one-wave register budget)
-  bool skinny_tiles = true;        // V^T projection (N = 48) on 64x64 tiles, one per block
-                                   // (ZV_GEMM_SKINNY=0: 128x64 persistent arm; a 128x96 tile for
-                                   // the N = 272 projection measured slower: profiles/r01_skinny_ab.txt)
-  bool defer_stores = false;       // A/B: ZV_GEMM_DEFER=1 lets the next tile's K loop run past the
-                                   // plain bf16 linears' stores (bitwise equal; up to 6 % in isolation,
-                                   // ~1 % slower in the model: profiles/r01_gemm_defer_ab.txt)
-  int res_counted = 31;            // A/B: ZV_RES_COUNTED=0 runs the residual linears through the
-                                   // (bit mask: 1 residual, 2 plain, 4 NA, 8 GLU, 16 transposed)
-                                   // general epilogue (zv_gemm.inc gemm_epilogue)
+  int res_counted = 31;            // ZV_RES_COUNTED: the counted epilogues (bit mask: 1 residual,
+                                   // 2 plain, 4 NA, 8 GLU, 16 transposed; 1 = all, 0 = the general
+                                   // epilogue, zv_gemm.inc gemm_epilogue: bitwise A/B tests)
   // ZV_GEMM256: the 256x256 phased kernel (zv_gemm256.inc) for the bias (+ SwooshL) and GLU
   // linears with at least gemm256_min_tiles tiles (1 persistent, 2 one tile per block, 0 off)
-  int gemm256 = 2, gemm256_min_tiles = 256;
-  bool biasnorm_v = true;          // ZV_BIASNORM_V: BiasNorm with every row load up front
-  // mixed (fp16 parity) mode: the SelfAttention Toeplitz table's lo half (ZV_MIXED_PLO=1) and the
-  // fp32 positional table for the head-0 / NonlinAttention scoring (ZV_MIXED_TPNA=0).  Both off
-  // by default: the full-size velocity error is unchanged at C2-C5 (C5 8.6e-4 either way) and
-  // the step 18 ms shorter (profiles/r03_mixed_ab.txt)
-  bool mixed_plo = false, mixed_tpna = true;
-  bool mixed_wsplit = true;        // ZV_MIXED_WSPLIT: the attention-score projection weight-split (0: bf16x3)
+  int gemm256 = 2;
   // ZV_MIXED_SA (fp16 parity mode): the SelfAttention value projection as a weight-split product and
   // its out-projection's residual update as a split product (the K-concatenated conv + SelfAttention
   // out-projection runs [dw | o_hi | o_lo | o_hi] . [conv_out | sa_out_hi | sa_out_hi | sa_out_lo]):
   // the families the emulation names for the random T = 203 input's 1.08e-3 -> 8.9e-4
   // (tools/precision_study.py --velocity, profiles/r04_precision_study_r04_velocity_T203.txt)
   bool mixed_sa = true;
-  bool pair_resid = false;         // A/B: ZV_PAIR_RESID=1 carries the bf16-mode residual stream as a
-                                   // bf16 hi/lo pair (8 B per update instead of 10): residual GEMMs
-                                   // -4..9 %, but the forward is unchanged (other kernels slower,
-                                   // profiles/r01_pair_resid_ab.txt); the fp32 stream stays default
+  // ZV_ATTN2 (bf16 / fp8 engines, default 1): second-generation attention consumers
+  // (zv_flash2.inc): log2(e) folded into the attention-score projection's k / p rows, the
+  // SelfAttention value projection padded to 16 rows per head (ones row 12), no statistics pass
+  bool attn_b2 = false;
 
   explicit zv_engine(const zv_config& c) : cfg(c) {
-    const char* e = getenv("ZV_ATTN_MATERIALIZE");
-    materialize_attn = e && e[0] == '1';
-    const char* gr = getenv("ZV_GRAPH");
-    graph_mode = gr ? atoi(gr) : 2;
-    const char* o1 = getenv("ZV_GEMM_OCC_PLAIN");
-    const char* o2 = getenv("ZV_GEMM_OCC_RESID");
-    const char* o3 = getenv("ZV_GEMM_OCC_FUSED");
-    occ_plain = o1 ? atoi(o1) : 2;
-    occ_resid = o2 ? atoi(o2) : 2;
-    occ_fused = o3 ? atoi(o3) : 2;
     auto envi = [](const char* k, int d) { const char* v = getenv(k); return v ? atoi(v) : d; };
-    gridx_plain = envi("ZV_GEMM_GRIDX_PLAIN", -1);
-    gridx_resid = envi("ZV_GEMM_GRIDX_RESID", -1);
-    gridx_fused = envi("ZV_GEMM_GRIDX_FUSED", -1);
+    materialize_attn = envi("ZV_ATTN_MATERIALIZE", 0) == 1;
+    graph_mode = envi("ZV_GRAPH", 2);
     sa_tp = envi("ZV_SA_TP", 1);
     fp8_fuse = envi("ZV_FP8_FUSE", 7);
-    kcat_sa = envi("ZV_KCAT_SA", 1) != 0;
-    sa_copy = envi("ZV_SA_COPY", 1) != 0;
-    n96_mode = envi("ZV_N96", 2);
-    ff1_src = envi("ZV_FF1_SRC", 1) != 0;
     ffn_fused = envi("ZV_FFN", 2);
     ffn_min_rows = envi("ZV_FFN_MIN_ROWS", 10000);
-    ffn_join = envi("ZV_FFN_JOIN", 0);
-    ffn_split_blocks = envi("ZV_FFN_SPLIT_BLOCKS", 0);
     ffn_persist = envi("ZV_FFN_PERSIST", 1);
-    skinny_tiles = envi("ZV_GEMM_SKINNY", 1) != 0;
-    defer_stores = envi("ZV_GEMM_DEFER", 0) != 0;
-    pair_resid = envi("ZV_PAIR_RESID", 0) != 0;
-    res_counted = envi("ZV_RES_COUNTED", 1) ? envi("ZV_RES_COUNTED_MASK", 31) : 0;
-    resid_ws = envi("ZV_RESID_WS", 0);
-    gemm_pp = envi("ZV_GEMM_PP", 0);
-    gemm_dual = envi("ZV_GEMM_DUAL", 0);
-#ifndef ZV_AB_KERNELS
-    ZV_REQUIRE(!gemm_pp && !gemm_dual && !resid_ws,
-               "ZV_GEMM_PP / ZV_GEMM_DUAL / ZV_RESID_WS need the A/B build (build.py -DZV_AB_KERNELS)");
-#endif
+    res_counted = envi("ZV_RES_COUNTED", 31);
+    if (res_counted == 1) res_counted = 31;
     split_streams = envi("ZV_SPLIT_STREAMS", 3);
     split_min_rows = envi("ZV_SPLIT_MIN_ROWS", 8192);
     gemm256 = envi("ZV_GEMM256", 2);
-    gemm256_min_tiles = envi("ZV_GEMM256_MIN_TILES", 256);
-    biasnorm_v = envi("ZV_BIASNORM_V", 1) != 0;
-    mixed_plo = envi("ZV_MIXED_PLO", 0) != 0;
-    mixed_tpna = envi("ZV_MIXED_TPNA", 1) != 0;
-    mixed_wsplit = envi("ZV_MIXED_WSPLIT", 1) != 0;
     mixed_sa = envi("ZV_MIXED_SA", 1) != 0;
+    attn_b2 = envi("ZV_ATTN2", 1) != 0 && (cfg.precision == ZV_BF16 || cfg.precision == ZV_FP8);
   }
   // the 256x256 kernel's preconditions (16-bit operands: the lo halves the fp32-accurate mode
   // keeps beside them are not read; padded K rows, the direct
@@ -423,152 +355,24 @@ struct zv_engine {
   bool io_split = false;           // set per decoder call: ZV_MIXED's split in/out projections
                                    // and attention-score projections
 
-  // ---------------------------------------------------------------- joined FeedForward
+  // ---------------------------------------------------------------- fused FeedForward sites
   // ZV_FFN_PERSIST (default 1): fused FeedForward launches on the persistent line schedule
-  // (zv_ffn.inc; results equal to one row block per block bit for bit).  ZV_FFN_JOIN (default 0:
-  // its cross-stream events cost more than the fill gains, bench 458-464 vs 417 ms):
-  // with the decoder's rows split over streams, the row blocks' FeedForward modules run as ONE
-  // launch over all rows: the line schedule needs the whole batch (C2 per stream: 204 row blocks
-  // for 256 CUs -- one round at best -- against 610 as one launch, 2.4 rounds of work in 2.42).
-  // The row blocks' host code runs as coroutines (ucontext) on the calling thread: each runs until
-  // its next FeedForward (recording an event on its stream), then the engine makes stream 0 wait
-  // for the others, launches once over the row ranges (FfnParams::seg), records an event the
-  // others wait for, and resumes them.  Every kernel stays on its row block's stream; only the
-  // FeedForward joins.
-  struct FfnCo {
-    struct Part {
-      ucontext_t ctx;
-      std::unique_ptr<char[]> stack;
-      std::function<void()> fn;
-      bool done = false, at_site = false;
-      std::exception_ptr err;
-      FfnParams q{};
-      hipStream_t s = nullptr;
-      const char* tag = nullptr;
-      int site = 0;
-    };
-    bool active = false, abort = false;
-    int n = 0, cur = 0;
-    Part part[MAX_SPLIT];
-    ucontext_t sched;
-    hipEvent_t ev_ready[MAX_SPLIT] = {}, ev_done = nullptr;
-  } co;
-  static constexpr size_t CO_STACK = 8u << 20;
-  int ffn_join = 0, ffn_persist = 1, ffn_split_blocks = 0;
-  int dec_parts = 0;               // row blocks of the split decoder while it runs (0: not split)
+  // (zv_ffn.inc; results equal to one row block per block bit for bit).  The scratch is sized for
+  // one line per CU; launch_ffn never launches more blocks than that (it checks)
+  int ffn_persist = 1;
   long dec_rows_N = 0;             // the whole batch's rows while a split decoder runs (0: not split):
                                    // the fused / unfused choice follows the batch, not the row block
-
-  static void co_entry(int lo, int hi) {
-    zv_engine* e = reinterpret_cast<zv_engine*>(((uintptr_t)(unsigned)hi << 32) | (uintptr_t)(unsigned)lo);
-    FfnCo::Part& pt = e->co.part[e->co.cur];
-    try {
-      pt.fn();
-    } catch (...) {
-      pt.err = std::current_exception();
-    }
-    pt.done = true;   // returns into co.sched (uc_link)
-  }
   void attach_ffn_scratch(FfnParams& q, Workspace& ws) {
     if (!ffn_persist) return;
     const int cus = zv_num_cus();
     q.part = ws.ffn_part.get<float>((size_t)cus * FFN_PART_FLOATS);
     unsigned* fl = ws.ffn_flag.get<unsigned>((size_t)cus + 64);
     q.flag = fl;
-    q.err = fl + cus + 32;
+    q.part_slots = cus;
   }
-  // one fused FeedForward launch, or this row block's range of the joined one
   void ffn_site(FfnParams q, Workspace& ws, hipStream_t s, const char* tag) {
-    if (co.active) {
-      FfnCo::Part& me = co.part[co.cur];
-      me.q = q; me.s = s; me.tag = tag; ++me.site; me.at_site = true;
-      if (co.cur > 0) ZV_CHECK(hipEventRecord(co.ev_ready[co.cur], s));
-      swapcontext(&me.ctx, &co.sched);
-      if (co.abort) throw std::runtime_error("split decoder aborted: another row block failed");
-      return;
-    }
     attach_ffn_scratch(q, ws);
-    // a row block's launch on the split decoder: lines over every CU (persistent only past one
-    // row block per CU).  ZV_FFN_SPLIT_BLOCKS caps a row block's launch at that many blocks (its
-    // share of the chip: C2 437 ms at 86 blocks, 424 at 128, 417 uncapped, profiles/r04_ffn_ab.txt)
-    const int bmax = (dec_parts > 1 && ffn_split_blocks > 0) ? ffn_split_blocks : 0;
-    launch_ffn(q, s, tag, bmax);
-  }
-  void ffn_join_launch() {
-    FfnCo::Part& p0 = co.part[0];
-    FfnParams q = p0.q;
-    q.nseg = co.n;
-    for (int i = 1; i < co.n; ++i) {
-      const FfnCo::Part& pi = co.part[i];
-      const FfnParams& o = pi.q;
-      ZV_REQUIRE(o.nseg == 1 && pi.site == p0.site && pi.tag == p0.tag && o.H == q.H && o.W1f == q.W1f &&
-                     o.W2f == q.W2f && o.b1 == q.b1 && o.b2 == q.b2 && o.byp == q.byp && o.nb == q.nb &&
-                     o.log_scale == q.log_scale && o.ldx == q.ldx && o.ldc == q.ldc && o.ldch == q.ldch &&
-                     o.rowvec_ld == q.rowvec_ld && o.rows_per_group == q.rows_per_group,
-                 "joined FeedForward: the row blocks reached different FeedForward launches");
-      q.seg[i] = o.seg[0];
-      ZV_CHECK(hipStreamWaitEvent(p0.s, co.ev_ready[i], 0));
-    }
-    attach_ffn_scratch(q, ws_dec);
-    launch_ffn(q, p0.s, p0.tag);
-    ZV_CHECK(hipEventRecord(co.ev_done, p0.s));
-    for (int i = 1; i < co.n; ++i) ZV_CHECK(hipStreamWaitEvent(co.part[i].s, co.ev_done, 0));
-  }
-  // run the row blocks' host code fn[0..n) as coroutines, joining them at every FeedForward
-  void run_joined(std::vector<std::function<void()>>& fns) {
-    co.n = (int)fns.size();
-    co.abort = false;
-    if (!co.ev_done) {
-      ZV_CHECK(ZV_BLOCKING(hipEventCreateWithFlags(&co.ev_done, hipEventDisableTiming)));
-      for (int i = 0; i < MAX_SPLIT; ++i) ZV_CHECK(ZV_BLOCKING(hipEventCreateWithFlags(&co.ev_ready[i], hipEventDisableTiming)));
-    }
-    for (int i = 0; i < co.n; ++i) {
-      FfnCo::Part& pt = co.part[i];
-      pt.fn = std::move(fns[i]);
-      pt.done = pt.at_site = false;
-      pt.err = nullptr;
-      pt.site = 0;
-      if (!pt.stack) pt.stack.reset(new char[CO_STACK]);
-      ZV_REQUIRE(getcontext(&pt.ctx) == 0, "getcontext");
-      pt.ctx.uc_stack.ss_sp = pt.stack.get();
-      pt.ctx.uc_stack.ss_size = CO_STACK;
-      pt.ctx.uc_link = &co.sched;
-      makecontext(&pt.ctx, (void (*)())co_entry, 2, (int)(unsigned)(uintptr_t)this,
-                  (int)(unsigned)((uintptr_t)this >> 32));
-    }
-    std::exception_ptr first;
-    co.active = true;
-    for (;;) {
-      for (int i = 0; i < co.n; ++i) {
-        FfnCo::Part& pt = co.part[i];
-        if (pt.done) continue;
-        co.cur = i;
-        pt.at_site = false;
-        swapcontext(&co.sched, &pt.ctx);
-      }
-      int ndone = 0, nsite = 0;
-      for (int i = 0; i < co.n; ++i) {
-        ndone += co.part[i].done;
-        nsite += co.part[i].at_site;
-        if (co.part[i].err && !first) first = co.part[i].err;
-      }
-      if (ndone == co.n) break;
-      if (first) { co.abort = true; continue; }          // resume the others: they unwind
-      if (nsite != co.n) {
-        first = std::make_exception_ptr(std::runtime_error("joined FeedForward: a row block finished early"));
-        co.abort = true;
-        continue;
-      }
-      try {
-        ffn_join_launch();
-      } catch (...) {
-        first = std::current_exception();
-        co.abort = true;
-      }
-    }
-    co.active = false;
-    for (int i = 0; i < co.n; ++i) co.part[i].fn = nullptr;
-    if (first) std::rethrow_exception(first);
+    launch_ffn(q, s, tag);
   }
 
   void drop_graphs() {
@@ -601,9 +405,6 @@ struct zv_engine {
     for (int i = 0; i < MAX_SPLIT - 1; ++i)
       if (split_join[i]) (void)ZV_BLOCKING(hipEventDestroy(split_join[i]));
     if (split_fork) (void)ZV_BLOCKING(hipEventDestroy(split_fork));
-    for (int i = 0; i < MAX_SPLIT; ++i)
-      if (co.ev_ready[i]) (void)ZV_BLOCKING(hipEventDestroy(co.ev_ready[i]));
-    if (co.ev_done) (void)ZV_BLOCKING(hipEventDestroy(co.ev_done));
     for (void* p : allocs) (void)ZV_BLOCKING(hipFree(p));
   }
 
@@ -616,12 +417,19 @@ struct zv_engine {
     return reinterpret_cast<T*>(p);
   }
   const std::vector<float>& take(const std::string& k, size_t numel) {
-    auto it = staged.find(k);
-    if (it == staged.end()) throw std::invalid_argument("missing weight: " + k);
-    if (it->second.size() != numel)
+    auto dt = derived.find(k);
+    const std::vector<float>* v = nullptr;
+    if (dt != derived.end()) {
+      v = &dt->second;
+    } else {
+      auto it = staged.find(k);
+      if (it == staged.end()) throw std::invalid_argument("missing weight: " + k);
+      v = &it->second;
+    }
+    if (v->size() != numel)
       throw std::invalid_argument("weight " + k + ": expected " + std::to_string(numel) +
-                                  " elements, got " + std::to_string(it->second.size()));
-    return it->second;
+                                  " elements, got " + std::to_string(v->size()));
+    return *v;
   }
   float* upload_f32(const std::string& k, size_t numel) {
     const auto& v = take(k, numel);
@@ -738,6 +546,38 @@ struct zv_engine {
       }
     return p;
   }
+  // staged copy of prefix.{weight, bias} with rows [r0, r1) multiplied by f (the second-generation
+  // attention's base-2 scores: log2(e) on the k and p rows of the attention-score projection)
+  std::string stage_rows_scaled(const std::string& prefix, int N, int K, int r0, int r1, float f) {
+    std::vector<float> w = take(prefix + ".weight", (size_t)N * K), b = take(prefix + ".bias", N);
+    for (int n = r0; n < r1; ++n) {
+      for (int k = 0; k < K; ++k) w[(size_t)n * K + k] *= f;
+      b[n] *= f;
+    }
+    const std::string np = prefix + "#b2";
+    derived[np + ".weight"] = std::move(w);
+    derived[np + ".bias"] = std::move(b);
+    return np;
+  }
+  // staged copy of a SelfAttention value projection (heads * vd rows) laid out 16 rows per head:
+  // [vd value rows | a zero row with bias 1 | zero rows]: its V^T carries the softmax denominator's
+  // ones row (zv_flash2.inc)
+  std::string stage_value_heads16(const std::string& prefix, int heads, int vd, int K) {
+    const auto& w = take(prefix + ".weight", (size_t)heads * vd * K);
+    const auto& b = take(prefix + ".bias", (size_t)heads * vd);
+    std::vector<float> w2((size_t)heads * 16 * K, 0.f), b2((size_t)heads * 16, 0.f);
+    for (int h = 0; h < heads; ++h) {
+      for (int d = 0; d < vd; ++d) {
+        memcpy(&w2[(size_t)(h * 16 + d) * K], &w[(size_t)(h * vd + d) * K], (size_t)K * sizeof(float));
+        b2[h * 16 + d] = b[h * vd + d];
+      }
+      b2[h * 16 + 12] = 1.f;
+    }
+    const std::string np = prefix + "#v16";
+    derived[np + ".weight"] = std::move(w2);
+    derived[np + ".bias"] = std::move(b2);
+    return np;
+  }
   Linear make_small(const std::string& prefix, int N, int K, bool bias) {
     Linear L;
     L.N = N; L.K = K;
@@ -787,7 +627,10 @@ struct zv_engine {
       for (int li = 0; li < layers[s]; ++li) {
         std::string lp = ep + "layers." + std::to_string(li) + ".";
         LayerW W;
-        W.attn_in = make_linear(lp + "self_attn_weights.in_proj", qkp, dim, true, false);
+        W.attn_in = make_linear(attn_b2 ? stage_rows_scaled(lp + "self_attn_weights.in_proj", qkp, dim,
+                                                            heads * Z.qd, qkp, 1.4426950408889634f)
+                                        : lp + "self_attn_weights.in_proj",
+                                qkp, dim, true, false);
         {
           const auto& pw = take(lp + "self_attn_weights.linear_pos.weight", pw_n);
           W.pos_w = S.pos_w_all + li * pw_n;
@@ -795,7 +638,13 @@ struct zv_engine {
         }
         for (int a = 0; a < 2; ++a) {
           std::string ap = lp + "self_attn" + std::to_string(a + 1) + ".";
-          W.sa_in[a] = make_linear(ap + "in_proj", heads * Z.vd, dim, true, false);
+          if (attn_b2) {
+            ZV_REQUIRE(Z.vd <= 12, "value_head_dim <= 12 for the padded value heads");
+            W.sa_in[a] = make_linear(stage_value_heads16(ap + "in_proj", heads, Z.vd, dim), heads * 16, dim,
+                                     true, false);
+          } else {
+            W.sa_in[a] = make_linear(ap + "in_proj", heads * Z.vd, dim, true, false);
+          }
           W.sa_out[a] = make_linear(ap + "out_proj", dim, heads * Z.vd, true, false);
         }
         const int hs[3] = {ff * 3 / 4, ff, ff * 5 / 4};
@@ -889,6 +738,7 @@ struct zv_engine {
                                   " tensors, config expects " + std::to_string(expected) +
                                   " (unexpected keys present)");
     staged.clear();
+    derived.clear();
     ready = true;
   }
 
@@ -1026,16 +876,6 @@ struct zv_engine {
       launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD>(p, 1, s, SPLIT == 3 ? "gemm_fp32_n64" : "gemm_bf16_n64");
       return false;
     }
-#ifdef ZV_AB_KERNELS
-    if constexpr (SPLIT == 1) {
-      if (gemm_pp && Lw.N % 128 == 0 && !o.act.l && !o.residh && A.ld % 8 == 0 &&
-          (!o.C || o.ldc % 8 == 0) && (!o.act.h || o.act.ld % 8 == 0)) {
-        if (o.resid) launch_gemm_pp<128, 128, 2, 4, EPI_STD, 1>(p, s, "gemm_bf16_resid");
-        else launch_gemm_pp<128, 128, 2, 4, EPI_STD, 0>(p, s, "gemm_bf16");
-        return false;
-      }
-    }
-#endif
     if constexpr (SPLIT == 1) {
       // bf16-only outputs on whole tiles: the next tile's K loop does not wait for
       // this tile's stores (counted vmcnt, zv_gemm.inc DEFER)
@@ -1047,16 +887,6 @@ struct zv_engine {
     }
     if (o.resid) {   // residual-stream linear: its own symbol / tag (HBM roofline)
       const char* rtag = SPLIT == 3 ? "gemm_fp32_resid" : "gemm_bf16_resid";   // ROLE 1
-#ifdef ZV_AB_KERNELS
-      if constexpr (SPLIT == 1)
-        if (gemm_dual && !o.act.l && Lw.K >= 64) {
-          GemmParams q = p;
-          if (gemm_dual_ok(q)) {       // two phase-offset tile groups per CU (zv_gemm_dual.inc)
-            launch_gemm_dual(q, s, "gemm_bf16_resid_dual");
-            return false;
-          }
-        }
-#endif
       if constexpr (SPLIT == 1) {
         // the copy-only form (no fp32 output) on the counted epilogue (A/B ZV_SA_COPY)
         if (sa_copy && !p.C && p.rowvec && !p.orig && !o.act.l && !o.act.q && p.Ch && p.bias &&
@@ -1065,17 +895,6 @@ struct zv_engine {
           else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 5>(p, 1, s, "gemm_bf16_resid_copy", true, gridx_resid);
           return false;
         }
-#ifdef ZV_AB_KERNELS
-        // wave-specialised epilogue (zv_gemm_ws.inc): faster where the linear is all epilogue
-        // (K <= 64: SelfAttention out-projections, -8 %); its single 4-wave MMA group per CU
-        // loses to zv_gemm_kernel's two co-resident blocks on longer K loops (+40 % at K = 1536,
-        // profiles/r01_resid_ws_ab.txt)
-        if (Lw.N % 128 == 0 && !o.act.l && (resid_ws == 2 || (resid_ws == 1 && Lw.K <= 64))) {
-          if (fp8_fuse & 1) { p.Cq = o.act.q; p.Cs = o.act.qs; p.ldcq = o.act.ldq; }
-          launch_gemm_resid_ws(p, s, "gemm_bf16_resid_ws");   // own tag: one symbol per roofline tag
-          return p.Cq != nullptr;
-        }
-#endif
       }
       // the counted residual epilogue (zv_gemm.inc gemm_epilogue_res; ROLE 2 = with the
       // bypass original) where its preconditions hold, else the general epilogue
@@ -1195,21 +1014,28 @@ struct zv_engine {
     // fallback for lengths whose fused LDS images do not fit) or keep only
     // per-row softmax statistics and recompute scores inside each consumer
     const int sa_plo = (SPLIT == 1 && sa_tp) ? (io_split && mixed_plo ? 1 : 0) : -1;
-    const bool materialize = materialize_attn || !fused_attn_fits<SPLIT>(L, W.na_in.N / 3, sa_plo, tp_na ? 1 : 0);
+    // second-generation consumers (zv_flash2.inc: base-2 scores from the log2(e)-scaled k / p
+    // weights, no running maximum, no statistics pass) wherever this engine's weights were
+    // built for them (attn_b2: bf16 / fp8 engines)
+    const bool a2 = SPLIT == 1 && attn_b2 && !io_split;
+    const bool materialize = materialize_attn || (a2 ? !fused_attn2_fits(L, W.na_in.N / 3)
+                                                     : !fused_attn_fits<SPLIT>(L, W.na_in.N / 3, sa_plo, tp_na ? 1 : 0));
     Act Wt;
     FlashParams fp{};
     if (materialize) {
       Wt = ws.W.get((long)H * M, Lpad, split);
-      AttnParams ap{qkp.h, qkp.l, qkpN, posP, pad, Wt.h, Wt.l, Lpad, B, L, H};
+      AttnParams ap{qkp.h, qkp.l, qkpN, posP, pad, Wt.h, Wt.l, Lpad, B, L, H, a2 ? 1 : 0};
       launch_attn_softmax<SPLIT>(ap, s);
     } else {
       fp.qh = qkp.h; fp.ql = qkp.l; fp.ldq = qkpN; fp.P = posP; fp.key_pad = pad;
-      fp.stats = ws.stats.get<float2>((size_t)M);     // head 0 only (NonlinAttention)
       fp.B = B; fp.L = L; fp.H = H;
-      if constexpr (SPLIT == 1)
-        if (tp_na) launch_attn_stats<1, 1>(fp, s);
-        else launch_attn_stats<1>(fp, s);
-      else launch_attn_stats<SPLIT>(fp, s);
+      if (!a2) {
+        fp.stats = ws.stats.get<float2>((size_t)M);     // head 0 only (NonlinAttention)
+        if constexpr (SPLIT == 1)
+          if (tp_na) launch_attn_stats<1, 1>(fp, s);
+          else launch_attn_stats<1>(fp, s);
+        else launch_attn_stats<SPLIT>(fp, s);
+      }
     }
     // fp8 mode: the working stream also carries an MX-fp8 copy (the A operand of the fp8
     // feed-forward / convolution in-projections), written by every producer of the stream:
@@ -1223,15 +1049,10 @@ struct zv_engine {
       if (!fresh8 || !(fp8_fuse & 4)) pack8(cur_a, M, D, s);
     }
     Out res;                       // cur = cur + module(cur), with the hi/lo copy
-    const bool pairm = SPLIT == 1 && pair_resid;
-    if (pairm) {                   // the stream itself is the (hi, lo) pair
-      res.residh = cur_a.h; res.residl = cur_a.l; res.act = cur_a;
-    } else {
-      res.C = cur; res.ldc = D; res.resid = cur; res.act = cur_a;
-    }
+    res.C = cur; res.ldc = D; res.resid = cur; res.act = cur_a;
     auto ff = [&](int f, const Out& oe) {
       if constexpr (SPLIT == 1) {
-        if (ffn_fused && W.ffn_w1f[f] && !pairm && !(f8 && W.ff_in[f].q8) && oe.C && oe.resid &&
+        if (ffn_fused && W.ffn_w1f[f] && !(f8 && W.ff_in[f].q8) && oe.C && oe.resid &&
             !oe.act.l && !oe.residh && Mtot >= ffn_min_rows && cur_a.ld % 8 == 0) {
           FfnParams q{};
           q.H = W.ff_in[f].N; q.nseg = 1;
@@ -1253,12 +1074,10 @@ struct zv_engine {
       linear<SPLIT>(W.ff_in[f], cur_a, M, o1, s);
       linear<SPLIT>(W.ff_out[f], hid, M, oe, s);
     };
-    if (pairm || !ff1_src) {
-      ff(0, res);                                     // FF1 (:536)
-    } else {
-      // FF1's residual is the layer input + the time embedding (src + temb, what the working
-      // stream holds on entry): read from src with the row vector, so neither BiasNorm nor
-      // the stack entry writes the fp32 working stream (only its bf16 / fp8 copies)
+    {
+      // FF1 (:536): its residual is the layer input + the time embedding (src + temb, what the
+      // working stream holds on entry): read from src with the row vector, so neither BiasNorm
+      // nor the stack entry writes the fp32 working stream (only its bf16 / fp8 copies)
       Out e1 = res;
       e1.resid = src;
       if (temb) { e1.rowvec = temb; e1.rowvec_ld = D; e1.rows_per_group = L; }
@@ -1272,10 +1091,6 @@ struct zv_engine {
       p.Ch = y.h; p.Cl = y.l; p.ldch = y.ld;
       p.Cth = xt.h; p.Ctl = xt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)hid * Lpad;
       bool done = false;
-#ifdef ZV_AB_KERNELS
-      if constexpr (SPLIT == 1)
-        if (gemm_pp && W.na_in.N % 192 == 0) { launch_gemm_pp<128, 192, 2, 4, EPI_NA, 0>(p, s, "gemm_bf16_na"); done = true; }
-#endif
       // counted NA epilogue: 16-bit modes (in the split mode it differs from the general one
       // by up to 1.1e-4 in the decoder output, tools/counted_bisect.py; not bitwise: kept off)
       if (done) {}
@@ -1302,7 +1117,12 @@ struct zv_engine {
         constexpr int QTILES = SPLIT == 3 ? 4 : 8;
         bool done = false;
         if constexpr (SPLIT == 1)
-          if (tp_na) {
+          if (a2) {
+            if (hid <= 128) launch_attn_na2<1>(f, s);
+            else if (hid <= 256) launch_attn_na2<2>(f, s);
+            else launch_attn_na2<3>(f, s);
+            done = true;
+          } else if (tp_na) {
             if (hid <= 128) launch_attn_na<1, 1, QTILES, 1>(f, s);
             else if (hid <= 256) launch_attn_na<1, 2, QTILES, 1>(f, s);
             else launch_attn_na<1, 3, QTILES, 1>(f, s);
@@ -1320,7 +1140,7 @@ struct zv_engine {
     // K = D + HV) and the convolution out-projection [conv_out | sa_out] finishes both residual
     // updates in one GEMM; the SelfAttention out-projection itself only writes the bf16 copy of
     // the stream the convolution module reads (cur + sa + temb: 6 B per element, not 10)
-    const bool kcat = SPLIT == 1 && kcat_sa && !f8 && !pairm && temb && W.conv_sa_out[0].hi &&
+    const bool kcat = SPLIT == 1 && !f8 && temb && W.conv_sa_out[0].hi &&
                       !materialize && (W.conv_sa_out[0].K == D + H * Z.vd || sa_tp);
     Act dwo;
     if (kcat) dwo = ws.dwo.get(M, round_up(W.conv_sa_out[0].K, 64), false);
@@ -1329,12 +1149,15 @@ struct zv_engine {
     ZV_REQUIRE(!kcat || sa_split || W.conv_sa_out[0].K == D + H * Z.vd, "conv + SelfAttention out-projection width");
     auto self_attn = [&](int a) {                     // SelfAttention (:564-570, :600-606)
       const int vd = Z.vd, HV = H * vd;
-      Act vt = ws.sa_vt.get((long)B * HV, Lpad, split);
+      // V^T rows per head: vd, or 16 where the value projection was built padded (sa_vpad: rows
+      // [12 values | ones | 3 zeros] per head, the second-generation kernel's operand)
+      const int VR = W.sa_in[a].N, vph = VR / H;
+      Act vt = ws.sa_vt.get((long)B * VR, Lpad, split);
       Act o = ws.sa_o.get(M, 64, split);
       if (kcat) { o = dwo; o.h += D; }               // columns [D, D + HV) of [dw | o]
       GemmParams p = gp_linear(W.sa_in[a], cur_a, M);
-      p.Cth = vt.h; p.Ctl = vt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)HV * Lpad;
-      // N = 48: 64-row tiles give 2x the blocks of a 128-row grid (one tile column)
+      p.Cth = vt.h; p.Ctl = vt.l; p.ldct = Lpad; p.rpb = L; p.sCt = (long)VR * Lpad;
+      // N = 48 (64 padded): 64-row tiles give 2x the blocks of a 128-row grid (one tile column)
       if (sa_split) {                    // fp16 parity mode: a . (w_hi + w_lo)
         ZV_REQUIRE(W.sa_in[a].lo && (res_counted & 16), "weight-split value projection");
         launch_gemm<64, 64, 2, 2, 2, EPI_TRANS, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, "gemm_wsplit_t", true, -1);
@@ -1346,19 +1169,24 @@ struct zv_engine {
         GemmParams q{};
         q.M = L; q.N = vd; q.K = L; q.nz2 = B; q.Brows = vd;
         q.Ah = Wt.h; q.Al = Wt.l; q.lda = Lpad; q.sA1 = M * Lpad; q.sA2 = (long)L * Lpad;
-        q.Bh = vt.h; q.Bl = vt.l; q.ldb = Lpad; q.sB1 = (long)vd * Lpad; q.sB2 = (long)HV * Lpad;
+        q.Bh = vt.h; q.Bl = vt.l; q.ldb = Lpad; q.sB1 = (long)vph * Lpad; q.sB2 = (long)VR * Lpad;
         q.Ch = o.h; q.Cl = o.l; q.ldch = o.ld; q.sCh1 = vd; q.sCh2 = (long)L * o.ld;
         q.rows_per_group = 1; q.rpb = 1;
         launch_gemm<128, 16, 4, 1, SPLIT, EPI_STD>(q, H * B, s, tag_att);
       } else {
         FlashParams f = fp;
-        f.vh = vt.h; f.vl = vt.l; f.ldv = Lpad; f.sv_b = (long)HV * Lpad; f.vrows_per_head = vd;
+        f.vh = vt.h; f.vl = vt.l; f.ldv = Lpad; f.sv_b = (long)VR * Lpad; f.vrows_per_head = vph;
         f.nv = vd;
         f.oh = o.h; f.ol = o.l; f.ldo = o.ld; f.ocol_per_head = vd;
         if (sa_split) { f.ol = o.h + HV; f.oh2 = o.h + 2 * HV; }   // [o_hi | o_lo | o_hi]
         bool done = false;
         if constexpr (SPLIT == 1)
-          if (sa_tp) {                   // positional term as a Toeplitz MFMA product
+          if (a2) {
+            // LDS-staged K / V (sa3) while two blocks fit a CU; the register-fed form past that
+            if (sa3_lds_bytes<2>(L) <= 80 * 1024) launch_attn_sa3<2>(f, s);
+            else launch_attn_sa2<2>(f, s);
+            done = true;
+          } else if (sa_tp) {            // positional term as a Toeplitz MFMA product
             if (sa_tp == 3) {          // A/B: the compiler's one-wave register budget
               if (io_split && mixed_plo) launch_attn_sa_tp<1, 1>(f, s);
               else launch_attn_sa_tp<0, 1>(f, s);
@@ -1384,10 +1212,6 @@ struct zv_engine {
         launch_gemm<128, 128, 2, 2, 8, EPI_GLU, 2, 2, MX8_KSTEP, 0, 0, 0, 3>(p, 1, s, "gemm_fp8_glu", true, gridx_fused);
         done = true;
       }
-#ifdef ZV_AB_KERNELS
-      if constexpr (SPLIT == 1)
-        if (gemm_pp && W.conv_in[c].N % 128 == 0) { launch_gemm_pp<128, 128, 2, 4, EPI_GLU, 0>(p, s, "gemm_bf16_glu"); done = true; }
-#endif
       if constexpr (SPLIT == 1)
         if (!done && (res_counted & 8) && p.bias && W.conv_in[c].N % 32 == 0 && p.ldch % 8 == 0 && use_gemm256(p)) {
           launch_gemm256<EPI_GLU, 3>(p, s, "gemm_bf16_glu", gemm256 == 1);
@@ -1415,15 +1239,14 @@ struct zv_engine {
     conv(0);                                          // conv1
     {                                                 // FF2 + bypass_mid (:593-598)
       Out e = res; e.byp = W.bypass_mid;
-      if (pairm) { e.origh = src_a.h; e.origl = src_a.l; }
-      else e.orig = src;
+      e.orig = src;
       ff(1, e);
     }
     self_attn(1);                                     // SA2 (+ temb)
     conv(1);                                          // conv2
     // FF3 + BiasNorm + bypass in the fused FeedForward kernel's norm epilogue (the FF3 output
     // never reaches HBM; zv_ffn.inc)
-    const bool ffn_norm = SPLIT == 1 && ffn_fused >= 2 && W.ffn_w1f[2] && !pairm && !f8 && D == FFN_D &&
+    const bool ffn_norm = SPLIT == 1 && ffn_fused >= 2 && W.ffn_w1f[2] && !f8 && D == FFN_D &&
                           Mtot >= ffn_min_rows && cur_a.ld == src_a.ld && cur_a.ld % 8 == 0;
     if (ffn_norm) {
       FfnParams q{};
@@ -1436,35 +1259,29 @@ struct zv_engine {
       q.byp = W.bypass; q.nb = W.norm_bias; q.log_scale = W.norm_log_scale;
       g.rowvec = temb; q.rowvec_ld = D; q.rows_per_group = L;
       g.C2h = has_next ? cur_a.h : nullptr; g.C2l = has_next ? cur_a.l : nullptr;
-      g.C2 = (has_next && !ff1_src) ? cur : nullptr;
+      g.C2 = nullptr;
       ffn_site(q, ws, s, "ffn_norm_bf16");
     } else {                                          // FF3: only the fp32 stream feeds BiasNorm
       Out e = res;                                    // (which rewrites both copies): no bf16 copy
-      if (!pairm) e.act = Act{};
+      e.act = Act{};
       ff(2, e);
     }
     // BiasNorm + bypass -> src; next layer's working copy (src + temb) -> cur
     if (ffn_norm) {
-    } else if (pairm) {   // pair stream; fp32 output only for the stack's last layer (next stack's input)
-      ZV_REQUIRE(D % 8 == 0 && cur_a.ld == src_a.ld, "pair-residual BiasNorm layout");
-      hipLaunchKernelGGL(zv_biasnorm_bypass_pair_kernel, dim3(cdiv(M, 4)), dim3(256), 0, s, cur_a.h,
-                         cur_a.l, src_a.h, src_a.l, src_a.ld, W.norm_bias, W.norm_log_scale, W.bypass,
-                         has_next ? nullptr : src, src_a.h, src_a.l, has_next ? cur_a.h : nullptr,
-                         has_next ? cur_a.l : nullptr, temb, L, M, D);
     } else {
       // fp8: the next layer's working stream's fp8 copy as well (its fresh8)
       const bool q2 = f8 && has_next && (fp8_fuse & 4);
       ZV_REQUIRE(!q2 || D % 256 == 0, "fp8 BiasNorm copy: channels a multiple of 256");
-      if (D == 512 && biasnorm_v)   // all loads of a row up front (ZV_BIASNORM_V=0: two-pass form)
+      if (D == 512)   // all loads of a row up front
         hipLaunchKernelGGL(zv_biasnorm_bypass_v_kernel<2>, dim3(cdiv(M, 8)), dim3(512), 0, s, cur, src,
                            W.norm_bias, W.norm_log_scale, W.bypass, src, src_a.h, src_a.l,
-                           ff1_src ? (float*)nullptr : cur, has_next ? cur_a.h : nullptr,
+                           (float*)nullptr, has_next ? cur_a.h : nullptr,
                            has_next ? cur_a.l : nullptr, (long)D, temb, L, M,
                            q2 ? c8.q : nullptr, q2 ? c8.qs : nullptr, q2 ? c8.ldq : 0L);
       else
         hipLaunchKernelGGL(zv_biasnorm_bypass_kernel, dim3(cdiv(M, 4)), dim3(256), 0, s, cur, src,
                            W.norm_bias, W.norm_log_scale, W.bypass, src, src_a.h, src_a.l,
-                           ff1_src ? (float*)nullptr : cur, has_next ? cur_a.h : nullptr,
+                           (float*)nullptr, has_next ? cur_a.h : nullptr,
                            has_next ? cur_a.l : nullptr,
                            (long)D, temb, L, M, D,
                            q2 ? c8.q : nullptr, q2 ? c8.qs : nullptr, q2 ? c8.ldq : 0L);
@@ -1478,12 +1295,11 @@ struct zv_engine {
              int L, const uint8_t* pad, const float* temb, hipStream_t s) {
     const long M = (long)B * L;
     const bool split = SPLIT == 3;
-    const bool pairm = SPLIT == 1 && pair_resid;
-    float* cur = pairm ? nullptr : ws.cur.get<float>(M * Z.dim);
-    Act cur_a = ws.cur_a.get(M, Z.dim, split || pairm);
+    float* cur = ws.cur.get<float>(M * Z.dim);
+    Act cur_a = ws.cur_a.get(M, Z.dim, split);
     // the fp32 working stream is not written here: the first layer's FF1 reads src + temb
     hipLaunchKernelGGL(zv_stack_entry_kernel, grid1d(M * Z.dim), dim3(256), 0, s, src, temb,
-                       (pairm || ff1_src) ? nullptr : cur, src_a.h, src_a.l, cur_a.h, cur_a.l, (long)Z.dim, M,
+                       (float*)nullptr, src_a.h, src_a.l, cur_a.h, cur_a.l, (long)Z.dim, M,
                        Z.dim, L);
     ZV_LAUNCH_CHECK();
     // positional encoding of length L and every layer's linear_pos projection of it, in one
@@ -1511,7 +1327,7 @@ struct zv_engine {
     // mixed mode: the input / output projections as split products (xin and the last
     // BiasNorm's copy main_a carry the lo halves)
     const bool ios = SPLIT == 1 && io_split;
-    Act main_a = ws.main_a.get(M, D, split || ios || (SPLIT == 1 && pair_resid));
+    Act main_a = ws.main_a.get(M, D, split || ios);
     {
       Out o; o.C = main; o.ldc = D;
       if (ios) linear<3>(Z.in_proj[sidx], xin, M, o, s);
@@ -1547,7 +1363,7 @@ struct zv_engine {
       } else {
         const int dL = (T + S.ds - 1) / S.ds;
         float* d = ws.dsrc.get<float>((size_t)N * dL * D);
-        Act d_a = ws.dsrc_a.get((long)N * dL, D, split || ios || (SPLIT == 1 && pair_resid));
+        Act d_a = ws.dsrc_a.get((long)N * dL, D, split || ios);
         hipLaunchKernelGGL(zv_downsample_kernel, grid1d((long)N * dL * D), dim3(256), 0, s, main, d,
                            N, T, dL, D, S.ds, S.ds_w);
         ZV_LAUNCH_CHECK();
@@ -1616,8 +1432,7 @@ struct zv_engine {
     // kernels of one block (GEMMs: MFMA/LDS) co-run with another block's (attention: VALU;
     // epilogues: HBM) instead of the whole batch passing each kernel in lock step.
     // Bitwise equal to the single-stream decoder (tests/test_gpu_split_streams.py): every kernel
-    // choice that depends on a row count takes the batch's (dec_rows_N), not the row block's, and
-    // the FeedForward modules run as one launch over all row blocks (run_joined).
+    // choice that depends on a row count takes the batch's (dec_rows_N), not the row block's.
     const int parts = std::min(split_streams, std::min(N, MAX_SPLIT));
     if (!split_fork) {
       ZV_CHECK(ZV_BLOCKING(hipEventCreateWithFlags(&split_fork, hipEventDisableTiming)));
@@ -1628,11 +1443,7 @@ struct zv_engine {
     }
     const int outN = dec.out_proj[sidx].N;
     ZV_CHECK(hipEventRecord(split_fork, s));
-    // the joined FeedForward (ffn_site) needs the row blocks' host code interleaved: coroutines
-    // on this thread (also under stream capture: the joins are event dependencies of the graph,
-    // and the warm-up run that sizes the workspace took the same path)
-    const bool join = ffn_join && ffn_fused && !g_zv_prof.on;
-    std::vector<std::function<void()>> fns;
+    dec_rows_N = N;   // every row block makes the batch's fused / unfused FeedForward choice
     int r0 = 0;
     for (int i = 0; i < parts; ++i) {
       const int n = N / parts + (i < N % parts ? 1 : 0);
@@ -1648,23 +1459,15 @@ struct zv_engine {
       const float* ti = t + r0;
       const float* gi = g ? g + r0 : nullptr;
       float* oi = out + rows * outN;
-      fns.push_back([this, wsi, xi, sidx, n, T, padi, ti, gi, oi, si]() {
+      try {
         decoder_rows(*wsi, xi, sidx, n, T, padi, ti, gi, oi, si);
-      });
+      } catch (...) {
+        dec_rows_N = 0;
+        throw;
+      }
       r0 += n;
     }
-    dec_rows_N = N;   // every row block makes the batch's fused / unfused FeedForward choice
-    dec_parts = join ? 0 : parts;
-    try {
-      if (join) run_joined(fns);
-      else for (auto& f : fns) f();
-    } catch (...) {
-      dec_rows_N = 0;
-      dec_parts = 0;
-      throw;
-    }
     dec_rows_N = 0;
-    dec_parts = 0;
     for (int i = 1; i < parts && !g_zv_prof.on; ++i) {
       ZV_CHECK(hipEventRecord(split_join[i - 1], split_stream[i - 1]));
       ZV_CHECK(hipStreamWaitEvent(s, split_join[i - 1], 0));
@@ -1896,22 +1699,6 @@ static float bench_variant(GemmParams p, int iters, bool persistent, hipStream_t
   return ms / iters;
 }
 
-#ifdef ZV_AB_KERNELS
-template <int BM, int BN, int WGM, int WGN, int EPI, int STAGES = 2>
-static float bench_variant_pp(GemmParams p, int iters, hipStream_t s) {
-  hipEvent_t e0, e1;
-  ZV_CHECK(ZV_BLOCKING(hipEventCreate(&e0))); ZV_CHECK(ZV_BLOCKING(hipEventCreate(&e1)));
-  launch_gemm_pp<BM, BN, WGM, WGN, EPI, 0, STAGES>(p, s, "bench");
-  ZV_CHECK(hipEventRecord(e0, s));
-  for (int i = 0; i < iters; ++i) launch_gemm_pp<BM, BN, WGM, WGN, EPI, 0, STAGES>(p, s, "bench");
-  ZV_CHECK(hipEventRecord(e1, s));
-  ZV_CHECK(ZV_BLOCKING(hipEventSynchronize(e1)));
-  float ms = 0.f;
-  ZV_CHECK(hipEventElapsedTime(&ms, e0, e1));
-  ZV_CHECK(ZV_BLOCKING(hipEventDestroy(e0))); ZV_CHECK(ZV_BLOCKING(hipEventDestroy(e1)));
-  return ms / iters;
-}
-#endif
 
 
 extern "C" {
@@ -1921,7 +1708,7 @@ const char* zv_last_error(void) { return g_last_error.c_str(); }
 #define ZV_SRC_HASH "unknown"
 #endif
 const char* zv_version(void) {
-  return "zipvoice_hip 0.3 (gfx950, " ZV_OPERAND_NAME " operands" ZV_AB_TAG ") src=" ZV_SRC_HASH;
+  return "zipvoice_hip 0.3 (gfx950, " ZV_OPERAND_NAME " operands" ") src=" ZV_SRC_HASH;
 }
 
 zv_handle zv_create(const zv_config* cfg) {
@@ -2087,11 +1874,6 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
     case 31: ms = bench_variant<128, 128, 2, 2, 3, 32>(p, iters, persistent, s); break;
     case 32: ms = bench_variant<256, 128, 2, 2, 2, 32>(p, iters, persistent, s); break;
     case 33: ms = bench_variant<256, 128, 2, 2, 3, 32>(p, iters, persistent, s); break;
-#ifdef ZV_AB_KERNELS
-    case 50: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD>(p, iters, s); break;
-    case 52: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD, 3>(p, iters, s); break;   // out mode 4 only
-    case 53: ms = bench_variant_pp<128, 128, 2, 4, EPI_STD, 4>(p, iters, s); break;   // out mode 4 only
-#endif
     case 72: {                     // counted plain epilogue (out mode 7)
       if (out_mode != 7) throw std::invalid_argument("variant 72: mode 7 only");
       ms = bench_variant<128, 128, 2, 2, 2, GEMM_BK, 0, 3>(p, iters, persistent, s);
@@ -2103,22 +1885,6 @@ int zv_bench_gemm(int M, int N, int K, int variant, int iters, int out_mode, flo
                          : bench_variant<128, 128, 2, 2, 2, GEMM_BK, 0, 2>(p, iters, persistent, s);
       break;
     }
-#ifdef ZV_AB_KERNELS
-    case 60: {                     // dual-group residual kernel (out mode 2 only)
-      if (out_mode != 2) throw std::invalid_argument("variant 60: residual mode only");
-      hipEvent_t e0, e1;
-      ZV_CHECK(ZV_BLOCKING(hipEventCreate(&e0))); ZV_CHECK(ZV_BLOCKING(hipEventCreate(&e1)));
-      launch_gemm_dual(p, s, "bench");
-      ZV_CHECK(hipEventRecord(e0, s));
-      for (int i = 0; i < iters; ++i) launch_gemm_dual(p, s, "bench");
-      ZV_CHECK(hipEventRecord(e1, s));
-      ZV_CHECK(ZV_BLOCKING(hipEventSynchronize(e1)));
-      ZV_CHECK(hipEventElapsedTime(&ms, e0, e1));
-      ms /= iters;
-      ZV_CHECK(ZV_BLOCKING(hipEventDestroy(e0))); ZV_CHECK(ZV_BLOCKING(hipEventDestroy(e1)));
-      break;
-    }
-#endif
     default: throw std::invalid_argument("unknown variant");
   }
   *ms_out = ms;
@@ -2155,9 +1921,16 @@ int zv_attn_plan(int split, int sa_plo, int tpm, int L, int nv_na, int64_t* lds_
                  int64_t* lds_stats, int* fits) {
   ZV_API_BEGIN
   ZV_REQUIRE((split == 1 || split == 3) && L > 0 && nv_na > 0 && sa_plo >= -1 && sa_plo <= 1 &&
-                 tpm >= 0 && tpm <= 2 && (split == 1 || (sa_plo < 0 && tpm == 0)) && lds_sa && lds_na &&
+                 tpm >= 0 && tpm <= 3 && (split == 1 || (sa_plo < 0 && tpm == 0)) && lds_sa && lds_na &&
                  lds_stats && fits,
              "bad arguments");
+  if (tpm == 3) {   // second-generation set (zv_flash2.inc): no statistics kernel
+    *lds_sa = (int64_t)(sa3_lds_bytes<2>(L) <= 80 * 1024 ? sa3_lds_bytes<2>(L) : sa2_lds_bytes<2>(L));
+    *lds_na = (int64_t)(nv_na <= 128 ? na2_lds_bytes<1, 8>(L) : nv_na <= 256 ? na2_lds_bytes<2, 8>(L) : na2_lds_bytes<3, 8>(L));
+    *lds_stats = 0;
+    *fits = fused_attn2_fits(L, nv_na);
+    return 0;
+  }
   *lds_sa = (int64_t)(sa_plo < 0 ? sa_lds_bytes(L) : (sa_plo ? sa_tp_lds_bytes<1>(L) : sa_tp_lds_bytes<0>(L)));
   *lds_na = (int64_t)(split == 1 ? na_lds_bytes_for<1>(L, nv_na, tpm) : na_lds_bytes_for<3>(L, nv_na, tpm));
   *lds_stats = (int64_t)pos_mask_bytes(L, 64, true);
@@ -2275,10 +2048,6 @@ int zv_gemm_selftest(int M, int N, int K, int variant, int mode, float* maxdiff,
     else switch (variant) {
       case 30: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 4, 2, 32>(p, 1, s, "t", true, 0); break;
       case 40: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2, GEMM_BK, 8>(p, 1, s, "t", true, 0); break;
-#ifdef ZV_AB_KERNELS
-      case 50: launch_gemm_pp<128, 128, 2, 4, EPI_STD, 0>(p, s, "t"); break;
-      case 60: case 61: launch_gemm_dual(p, s, "t"); break;
-#endif
       // the counted residual epilogue (ROLE 1 / 2) against the general one
       case 70: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 1>(p, 1, s, "t", true, -1); break;
       case 71: launch_gemm<128, 128, 2, 2, 1, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 2>(p, 1, s, "t", true, -1); break;
