@@ -60,13 +60,17 @@ def test_split_streams_bitwise(monkeypatch, variant, precision, parts):
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp16"])
-def test_ffn_persistent_and_joined_bitwise(monkeypatch, precision):
+def test_ffn_persistent_bitwise(monkeypatch, precision):
     """The fused FeedForward's persistent line schedule (ZV_FFN_PERSIST, zv_ffn.inc: row blocks cut
-    into P / C items whose out^T tiles are handed over through memory) and the joined launch over
-    the split decoder's row blocks (ZV_FFN_JOIN: one launch, one row range per stream) against one
-    row block per block on one stream, with the default thresholds: bitwise equal velocities.
+    into P / C items whose out^T tiles are handed over through memory, one flag word per line)
+    against one row block per block, on one stream and on the split decoder's three streams, with
+    the default thresholds: bitwise equal velocities.
     16 utterances = 32 CFG rows x 1219 frames: 39008 rows (305 row blocks) at the full-rate stacks,
-    19504 at the half-rate ones -- lines cut row blocks at every stack that runs fused."""
+    19504 at the half-rate ones -- lines cut row blocks at every stack that runs fused.
+    Two different velocities run back to back on each engine (and every call launches the kernel
+    48 times on one scratch): a flag word left set by one launch would let the next launch's C
+    item skip its wait and start from the previous launch's tiles -- the second output would then
+    differ (the round-4 hand-off faults, DESIGN.md §3, were of this family)."""
     from zipvoice_amd.config import default_config
     from zipvoice_amd.models import build_model
     from zipvoice_amd.weights import synthetic_state_dict
@@ -77,9 +81,8 @@ def test_ffn_persistent_and_joined_bitwise(monkeypatch, precision):
     outs = []
     for env in ({"ZV_SPLIT_STREAMS": "1", "ZV_FFN_PERSIST": "0"},
                 {"ZV_SPLIT_STREAMS": "1", "ZV_FFN_PERSIST": "1"},
-                {"ZV_SPLIT_STREAMS": "3", "ZV_FFN_JOIN": "1", "ZV_FFN_PERSIST": "1"},
-                {"ZV_SPLIT_STREAMS": "3", "ZV_FFN_JOIN": "0", "ZV_FFN_PERSIST": "1"}):
-        for k in ("ZV_SPLIT_STREAMS", "ZV_FFN_JOIN", "ZV_FFN_PERSIST", "ZV_FFN_MIN_ROWS", "ZV_GRAPH"):
+                {"ZV_SPLIT_STREAMS": "3", "ZV_FFN_PERSIST": "1"}):
+        for k in ("ZV_SPLIT_STREAMS", "ZV_FFN_PERSIST", "ZV_FFN_MIN_ROWS", "ZV_GRAPH"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)

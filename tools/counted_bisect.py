@@ -1,4 +1,4 @@
-"""Which counted epilogue class changes the fp32-mode decoder output (ZV_RES_COUNTED_MASK bits:
+"""Which counted epilogue class changes the fp32-mode decoder output (ZV_RES_COUNTED bits:
 1 residual, 2 plain, 4 NA, 8 GLU, 16 transposed)?  Runs each single class against none."""
 import os
 import subprocess
@@ -22,7 +22,7 @@ prec = sys.argv[1] if len(sys.argv) > 1 else "fp32"
 import numpy as np
 res = {}
 for mask in (0, 1, 2, 4, 8, 16, 31):
-    env = dict(os.environ, ZV_RES_COUNTED_MASK=str(mask))
+    env = dict(os.environ, ZV_RES_COUNTED=str(mask) if mask != 1 else "31")
     out = f"gpurun_out/cb_{prec}_{mask}.npy"
     subprocess.run([sys.executable, "-c", CODE, prec, out], env=env, check=True, timeout=300)
     res[mask] = np.load(out)
