@@ -22,7 +22,7 @@ prec = sys.argv[1] if len(sys.argv) > 1 else "fp32"
 import numpy as np
 res = {}
 for mask in (0, 1, 2, 4, 8, 16, 31):
-    env = dict(os.environ, ZV_RES_COUNTED=str(mask) if mask != 1 else "31")
+    env = dict(os.environ, ZV_RES_COUNTED=str(32 + mask))
     out = f"gpurun_out/cb_{prec}_{mask}.npy"
     subprocess.run([sys.executable, "-c", CODE, prec, out], env=env, check=True, timeout=300)
     res[mask] = np.load(out)

@@ -255,10 +255,18 @@ int main(int argc, char** argv) {
         FlashParams n3 = n2; n3.qh = q3;
         launch_attn_sa2<2>(f3, s);
         launch_attn_na2<3>(n3, s);
+        launch_attn_sa3<2>(f3, s);
         ZV_CHECK(hipStreamSynchronize(s));
         printf("  exact paths ran (large scores)\n");
         timeit("sa2-exact", H * (72.0 + 2.0 * VD), [&] { launch_attn_sa2<2>(f3, s); });
         timeit("na2-exact", 72.0 + 2.0 * HID, [&] { launch_attn_na2<3>(n3, s); });
+        // exactness: the v3 exact paths against the v2 exact paths on the same (large) scores
+        FlashParams f4 = f3; f4.oh = u.o_sa;
+        launch_attn_sa3<2>(f4, s);
+        launch_attn_sa2<2>(f3, s);
+        ZV_CHECK(hipStreamSynchronize(s));
+        cmp("sa3x-sa2x", u.o_sa, u.o_sa2, 64, HV);
+        timeit("sa3-exact", H * (72.0 + 2.0 * VD), [&] { launch_attn_sa3<2>(f3, s); });
         ZV_CHECK(hipFree(q3));
       }
     }

@@ -278,7 +278,8 @@ struct zv_engine {
                                    // (3: A/B arm, SA with the one-wave register budget)
   int res_counted = 31;            // ZV_RES_COUNTED: the counted epilogues (bit mask: 1 residual,
                                    // 2 plain, 4 NA, 8 GLU, 16 transposed; 1 = all, 0 = the general
-                                   // epilogue, zv_gemm.inc gemm_epilogue: bitwise A/B tests)
+                                   // epilogue, zv_gemm.inc gemm_epilogue: bitwise A/B tests;
+                                   // 32 + mask: that mask)
   // ZV_GEMM256: the 256x256 phased kernel (zv_gemm256.inc) for the bias (+ SwooshL) and GLU
   // linears with at least gemm256_min_tiles tiles (1 persistent, 2 one tile per block, 0 off)
   int gemm256 = 2;
@@ -303,7 +304,8 @@ struct zv_engine {
     ffn_min_rows = envi("ZV_FFN_MIN_ROWS", 10000);
     ffn_persist = envi("ZV_FFN_PERSIST", 1);
     res_counted = envi("ZV_RES_COUNTED", 31);
-    if (res_counted == 1) res_counted = 31;
+    if (res_counted == 1) res_counted = 31;            // 1: all (0 / 1 are the A/B tests' arms)
+    else if (res_counted >= 32) res_counted &= 31;     // 32 + mask: exactly that mask (bisection)
     split_streams = envi("ZV_SPLIT_STREAMS", 3);
     split_min_rows = envi("ZV_SPLIT_MIN_ROWS", 8192);
     gemm256 = envi("ZV_GEMM256", 2);
