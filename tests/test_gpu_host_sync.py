@@ -76,6 +76,9 @@ def test_warm_step_has_no_host_block(monkeypatch, split):
         c1 = engine.host_block_count()
     finally:
         gc.enable()
+        # (the sample wrapper switched the mode on; a raise before the decode wrapper's finally
+        # would leave every later test's first .item() failing)
+        torch.cuda.set_sync_debug_mode("default")
     torch.cuda.synchronize()
     print(f"split={split}: host-blocking engine calls in a warm step {c1 - c0} "
           f"(solver entry -> vocoder return {inner['c1'] - inner['c0']}); torch sync guard "
