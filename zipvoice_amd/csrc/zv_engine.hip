@@ -190,17 +190,17 @@ static StreamSet acquire_stream_set() {
         return set;
       }
   }
+  // (the streams themselves are created on first use, engine_stream: a process holds only the
+  // streams its engines launch on -- the caller's + split_streams - 1, + 1 for graph replay --
+  // against its GPU_MAX_HW_QUEUES (4) hardware queues)
   StreamSet set;
   set.dev = dev;
-  // (row-block streams at the greatest / least priority lost 1.9 % / 0.6 % per C2 step, round 4:
-  // profiles/r04_stream_prio.txt; all streams at the default priority)
-  for (int i = 0; i < ZV_STREAM_SET; ++i)
-    ZV_CHECK(ZV_BLOCKING(hipStreamCreateWithFlags(&set.s[i], hipStreamNonBlocking)));
   return set;
 }
 static void release_stream_set(const StreamSet& set) {
   if (set.dev < 0) return;
-  for (hipStream_t st : set.s) (void)ZV_BLOCKING(hipStreamSynchronize(st));
+  for (hipStream_t st : set.s)
+    if (st) (void)ZV_BLOCKING(hipStreamSynchronize(st));
   std::lock_guard<std::mutex> lock(g_stream_pool_mu);
   stream_pool_free().push_back(set);
 }
@@ -395,6 +395,9 @@ struct zv_engine {
   hipStream_t engine_stream(int slot) {
     static_assert(MAX_SPLIT <= ZV_STREAM_SET, "stream set holds the split streams and the graph stream");
     if (streams.dev < 0) streams = acquire_stream_set();
+    // (row-block streams at the greatest / least priority lost 1.9 % / 0.6 % per C2 step, round 4:
+    // profiles/r04_stream_prio.txt; all streams at the default priority)
+    if (!streams.s[slot]) ZV_CHECK(ZV_BLOCKING(hipStreamCreateWithFlags(&streams.s[slot], hipStreamNonBlocking)));
     return streams.s[slot];
   }
 
@@ -1438,11 +1441,11 @@ struct zv_engine {
     const int parts = std::min(split_streams, std::min(N, MAX_SPLIT));
     if (!split_fork) {
       ZV_CHECK(ZV_BLOCKING(hipEventCreateWithFlags(&split_fork, hipEventDisableTiming)));
-      for (int i = 0; i < MAX_SPLIT - 1; ++i) {
-        split_stream[i] = engine_stream(i);
+      for (int i = 0; i < MAX_SPLIT - 1; ++i)
         ZV_CHECK(ZV_BLOCKING(hipEventCreateWithFlags(&split_join[i], hipEventDisableTiming)));
-      }
     }
+    for (int i = 1; i < parts; ++i)   // (only the streams this split uses)
+      if (!split_stream[i - 1]) split_stream[i - 1] = engine_stream(i - 1);
     const int outN = dec.out_proj[sidx].N;
     ZV_CHECK(hipEventRecord(split_fork, s));
     dec_rows_N = N;   // every row block makes the batch's fused / unfused FeedForward choice
