@@ -62,13 +62,13 @@ HBM_PEAK_GBS = 8000.0
 # the engine's profiler tag (one symbol per tag since round 3: the residual linears by ROLE, the
 # fused FeedForward with / without the BiasNorm epilogue); newest measurement first
 # (round 4: measured on the timed three-stream schedule, the same launch set the roofline pass times)
-TRAFFIC_FILES = {"gemm_bf16_resid": ["r04_gemm_resid_r1_traffic.json", "r03_gemm_resid_r1_traffic.json"],
-                 "gemm_bf16_resid_rv": ["r04_gemm_resid_r4_traffic.json", "r03_gemm_resid_r4_traffic.json"],
-                 "gemm_bf16_resid_byp": ["r04_gemm_resid_r2_traffic.json", "r03_gemm_resid_r2_traffic.json"],
-                 "ffn_bf16": ["r04_ffn_traffic.json", "r03_ffn_traffic.json"],
-                 "ffn_norm_bf16": ["r04_ffn_norm_traffic.json", "r03_ffn_norm_traffic.json"],
-                 "ffn_bf16+ffn_norm_bf16": ["r04_ffn_all_traffic.json"],
-                 "gemm_bf16": ["r04_gemm_traffic.json", "r03_gemm_traffic.json"]}
+TRAFFIC_FILES = {"gemm_bf16_resid": ["r05_gemm_resid_r1_traffic.json", "r04_gemm_resid_r1_traffic.json"],
+                 "gemm_bf16_resid_rv": ["r05_gemm_resid_r4_traffic.json", "r04_gemm_resid_r4_traffic.json"],
+                 "gemm_bf16_resid_byp": ["r05_gemm_resid_r2_traffic.json", "r04_gemm_resid_r2_traffic.json"],
+                 "ffn_bf16": ["r05_ffn_traffic.json", "r04_ffn_traffic.json"],
+                 "ffn_norm_bf16": ["r05_ffn_norm_traffic.json", "r04_ffn_norm_traffic.json"],
+                 "ffn_bf16+ffn_norm_bf16": ["r05_ffn_all_traffic.json", "r04_ffn_all_traffic.json"],
+                 "gemm_bf16": ["r05_gemm_traffic.json", "r04_gemm_traffic.json"]}
 # the residual-stream linears by epilogue ROLE (zv_gemm.inc): the HBM-bound family of the path
 RESID_TAGS = ("gemm_bf16_resid", "gemm_bf16_resid_rv", "gemm_bf16_resid_byp")
 # analytic FLOPs of one decoder sequence-forward (FlopCounterMode fit on the
