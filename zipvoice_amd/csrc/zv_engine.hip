@@ -190,11 +190,14 @@ static StreamSet acquire_stream_set() {
         return set;
       }
   }
-  // (the streams themselves are created on first use, engine_stream: a process holds only the
-  // streams its engines launch on -- the caller's + split_streams - 1, + 1 for graph replay --
-  // against its GPU_MAX_HW_QUEUES (4) hardware queues)
+  // (the whole set up front: creating the streams on first use instead -- a process then holds
+  // only the streams it launches on -- left one engine alone equal but put a later engine of the
+  // same process on a worse queue mapping: the bench's fp32 leg 991 -> 1087 ms,
+  // profiles/r05_streams_ab.txt)
   StreamSet set;
   set.dev = dev;
+  for (int i = 0; i < ZV_STREAM_SET; ++i)
+    ZV_CHECK(ZV_BLOCKING(hipStreamCreateWithFlags(&set.s[i], hipStreamNonBlocking)));
   return set;
 }
 static void release_stream_set(const StreamSet& set) {
