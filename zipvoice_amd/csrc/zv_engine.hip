@@ -1193,8 +1193,12 @@ struct zv_engine {
         if constexpr (SPLIT == 1)
           if (a2) {
             // LDS-staged K / V (sa3) while two blocks fit a CU; the register-fed form past that
-            if (sa3_pick(L)) launch_attn_sa3<2>(f, s);
-            else launch_attn_sa2<2>(f, s);
+            switch (sa3_qpw(L)) {
+              case 4: launch_attn_sa3<4>(f, s); break;
+              case 3: launch_attn_sa3<3>(f, s); break;
+              case 2: launch_attn_sa3<2>(f, s); break;
+              default: launch_attn_sa2<2>(f, s);
+            }
             done = true;
           } else if (sa_tp) {            // positional term as a Toeplitz MFMA product
             if (sa_tp == 3) {          // A/B: the compiler's one-wave register budget
@@ -1935,7 +1939,7 @@ int zv_attn_plan(int split, int sa_plo, int tpm, int L, int nv_na, int64_t* lds_
                  lds_stats && fits,
              "bad arguments");
   if (tpm == 3) {   // second-generation set (zv_flash2.inc): no statistics kernel
-    *lds_sa = (int64_t)(sa3_pick(L) ? sa3_lds_bytes<2>(L) : sa2_lds_bytes<2>(L));
+    *lds_sa = (int64_t)(sa3_qpw(L) ? sa3_plan_lds(L) : sa2_lds_bytes<2>(L));
     *lds_na = (int64_t)(nv_na <= 128 ? na2_lds_bytes<1, 8>(L) : nv_na <= 256 ? na2_lds_bytes<2, 8>(L) : na2_lds_bytes<3, 8>(L));
     *lds_stats = 0;
     *fits = fused_attn2_fits(L, nv_na);
