@@ -200,6 +200,24 @@ int main(int argc, char** argv) {
         cmp("sa3q1", u.o_sa2, u.o_sa, 64, HV);
         timeit("sa3q1", H * (72.0 + 2.0 * VD), [&] { launch_attn_sa3<1, 4>(f2, s); });
       }
+      if (on("sa2q")) {   // the register-fed form with more query tiles per wave (long sequences)
+        launch_attn_sa2<3, 1>(f2, s);
+        ZV_CHECK(hipStreamSynchronize(s));
+        cmp("sa2q3", u.o_sa2, u.o_sa, 64, HV);
+        timeit("sa2q3", H * (72.0 + 2.0 * VD), [&] { launch_attn_sa2<3, 1>(f2, s); });
+        launch_attn_sa2<4, 1>(f2, s);
+        ZV_CHECK(hipStreamSynchronize(s));
+        cmp("sa2q4", u.o_sa2, u.o_sa, 64, HV);
+        timeit("sa2q4", H * (72.0 + 2.0 * VD), [&] { launch_attn_sa2<4, 1>(f2, s); });
+        launch_attn_sa3<4, 1>(f2, s);
+        ZV_CHECK(hipStreamSynchronize(s));
+        cmp("sa3q4w1", u.o_sa2, u.o_sa, 64, HV);
+        timeit("sa3q4w1", H * (72.0 + 2.0 * VD), [&] { launch_attn_sa3<4, 1>(f2, s); });
+        launch_attn_sa3<3, 1>(f2, s);
+        ZV_CHECK(hipStreamSynchronize(s));
+        cmp("sa3q3w1", u.o_sa2, u.o_sa, 64, HV);
+        timeit("sa3q3w1", H * (72.0 + 2.0 * VD), [&] { launch_attn_sa3<3, 1>(f2, s); });
+      }
       if (on("sa3q")) {   // more query tiles per wave (K / V / Toeplitz reads shared by more tiles)
         launch_attn_sa3<3, 2>(f2, s);
         ZV_CHECK(hipStreamSynchronize(s));

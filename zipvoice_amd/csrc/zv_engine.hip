@@ -1197,7 +1197,9 @@ struct zv_engine {
               case 4: launch_attn_sa3<4>(f, s); break;
               case 3: launch_attn_sa3<3>(f, s); break;
               case 2: launch_attn_sa3<2>(f, s); break;
-              default: launch_attn_sa2<2>(f, s);
+              default:
+                if (sa2_qpw(L) == 3) launch_attn_sa2<3, 1>(f, s);
+                else launch_attn_sa2<2>(f, s);
             }
             done = true;
           } else if (sa_tp) {            // positional term as a Toeplitz MFMA product
@@ -1939,7 +1941,7 @@ int zv_attn_plan(int split, int sa_plo, int tpm, int L, int nv_na, int64_t* lds_
                  lds_stats && fits,
              "bad arguments");
   if (tpm == 3) {   // second-generation set (zv_flash2.inc): no statistics kernel
-    *lds_sa = (int64_t)(sa3_qpw(L) ? sa3_plan_lds(L) : sa2_lds_bytes<2>(L));
+    *lds_sa = (int64_t)(sa3_qpw(L) ? sa3_plan_lds(L) : sa2_qpw(L) == 3 ? sa2_lds_bytes<3>(L) : sa2_lds_bytes<2>(L));
     *lds_na = (int64_t)(nv_na <= 128 ? na2_lds_bytes<1, 8>(L) : nv_na <= 256 ? na2_lds_bytes<2, 8>(L) : na2_lds_bytes<3, 8>(L));
     *lds_stats = 0;
     *fits = fused_attn2_fits(L, nv_na);
