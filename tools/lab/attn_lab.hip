@@ -273,6 +273,12 @@ int main(int argc, char** argv) {
         cmp("na2", u.o_na2, u.o_na, HID, HID);
         timeit("na2", 72.0 + 2.0 * HID, [&] { launch_attn_na2<3>(n2, s); });
       }
+      if (on("na2q")) {   // 4 query tiles per block (8 waves)
+        launch_attn_na2<3, 4>(n2, s);
+        ZV_CHECK(hipStreamSynchronize(s));
+        cmp("na2q4", u.o_na2, u.o_na, HID, HID);
+        timeit("na2q4", 72.0 + 2.0 * HID, [&] { launch_attn_na2<3, 4>(n2, s); });
+      }
       // the exact (fallback) paths: scores pushed past the no-maximum range (every q scaled by
       // 2^6 -> |scores| ~ 2^7: the range check must fail and the exact path take over)
       if (on("exact")) {

@@ -1126,8 +1126,10 @@ struct zv_engine {
         bool done = false;
         if constexpr (SPLIT == 1)
           if (a2) {
-            if (hid <= 128) launch_attn_na2<1>(f, s);
-            else if (hid <= 256) launch_attn_na2<2>(f, s);
+            const bool q4 = na2_qtiles(L) == 4;
+            if (hid <= 128) { if (q4) launch_attn_na2<1, 4>(f, s); else launch_attn_na2<1>(f, s); }
+            else if (hid <= 256) { if (q4) launch_attn_na2<2, 4>(f, s); else launch_attn_na2<2>(f, s); }
+            else if (q4) launch_attn_na2<3, 4>(f, s);
             else launch_attn_na2<3>(f, s);
             done = true;
           } else if (tp_na) {
