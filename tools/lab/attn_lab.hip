@@ -200,6 +200,16 @@ int main(int argc, char** argv) {
         cmp("sa3q1", u.o_sa2, u.o_sa, 64, HV);
         timeit("sa3q1", H * (72.0 + 2.0 * VD), [&] { launch_attn_sa3<1, 4>(f2, s); });
       }
+      if (on("sa2s")) {   // short sequences: fewer query tiles per wave (more blocks)
+        launch_attn_sa2<1, 4>(f2, s);
+        ZV_CHECK(hipStreamSynchronize(s));
+        cmp("sa2q1", u.o_sa2, u.o_sa, 64, HV);
+        timeit("sa2q1", H * (72.0 + 2.0 * VD), [&] { launch_attn_sa2<1, 4>(f2, s); });
+        launch_attn_sa3<1, 4>(f2, s);
+        ZV_CHECK(hipStreamSynchronize(s));
+        cmp("sa3q1", u.o_sa2, u.o_sa, 64, HV);
+        timeit("sa3q1", H * (72.0 + 2.0 * VD), [&] { launch_attn_sa3<1, 4>(f2, s); });
+      }
       if (on("sa2q")) {   // the register-fed form with more query tiles per wave (long sequences)
         launch_attn_sa2<3, 1>(f2, s);
         ZV_CHECK(hipStreamSynchronize(s));
