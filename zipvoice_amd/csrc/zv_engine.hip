@@ -153,8 +153,13 @@ struct Workspace {
   // the fused FeedForward's persistent schedule (zv_ffn.inc): one 256 KiB tile slot per CU, one
   // flag word per CU (zero between launches) and the spin-timeout counter
   DBuf ffn_part, ffn_flag;
+  // per-stack positional projections, kept across the Euler steps of one solve (they depend on
+  // the stack's length and weights only; Engine::posp_reuse)
+  static constexpr int POSP_STACKS = 8;
+  DBuf posPs[POSP_STACKS];
   size_t bytes() const {
     size_t s = 0;
+    for (const DBuf& b : posPs) s += b.bytes;
     for (const DBuf* b : {&main, &dsrc, &cur, &temb0, &temb1, &tstack, &tvec, &gvec, &posP, &mask2,
                           &maskds, &vout, &stats, &ffn_part, &ffn_flag})
       s += b->bytes;
@@ -357,6 +362,7 @@ struct zv_engine {
   // cross-branch waits), while single-stream shapes (one sentence) are launch-bound and
   // need the graph
   int graph_mode = 2;
+  bool posp_reuse = false;         // euler_loop: the stacks' posP buffers hold this solve's values
   bool io_split = false;           // set per decoder call: ZV_MIXED's split in/out projections
                                    // and attention-score projections
 
@@ -1309,7 +1315,7 @@ struct zv_engine {
 
   // ---------------------------------------------------------------- one stack
   template <int SPLIT>
-  void stack(const ZipformerW& Z, const StackW& S, Workspace& ws, float* src, Act src_a, int B,
+  void stack(const ZipformerW& Z, const StackW& S, int si, Workspace& ws, float* src, Act src_a, int B,
              int L, const uint8_t* pad, const float* temb, hipStream_t s) {
     const long M = (long)B * L;
     const bool split = SPLIT == 3;
@@ -1322,12 +1328,18 @@ struct zv_engine {
     ZV_LAUNCH_CHECK();
     // positional encoding of length L and every layer's linear_pos projection of it, in one
     // launch into the workspace (zipformer.py:983-1056, :1239): no host table, no cache, no
-    // synchronisation, graph-capturable
+    // synchronisation, graph-capturable.  It depends on L and the stack's weights only: inside
+    // one Euler solve the first step writes it into the stack's own buffer and the later steps
+    // (same rows, same L, same workspace per row block) read it again (posp_reuse)
     const int R = 2 * L - 1, HPD = Z.heads * Z.pd, nl = (int)S.layers.size();
-    float* posP = ws.posP.get<float>((size_t)std::max(nl, 1) * R * HPD);
-    hipLaunchKernelGGL(zv_posp_kernel, dim3((unsigned)cdiv((long)nl * R * HPD, 256L)), dim3(256), 0, s, S.pos_w_all, posP,
-                       L, nl, HPD, Z.pos_dim);
-    ZV_LAUNCH_CHECK();
+    const size_t pn = (size_t)std::max(nl, 1) * R * HPD;
+    const bool own = si >= 0 && si < Workspace::POSP_STACKS;
+    float* posP = own ? ws.posPs[si].get<float>(pn) : ws.posP.get<float>(pn);
+    if (!(own && posp_reuse)) {
+      hipLaunchKernelGGL(zv_posp_kernel, dim3((unsigned)cdiv((long)nl * R * HPD, 256L)), dim3(256), 0, s, S.pos_w_all, posP,
+                         L, nl, HPD, Z.pos_dim);
+      ZV_LAUNCH_CHECK();
+    }
     for (size_t li = 0; li < S.layers.size(); ++li)
       layer<SPLIT>(Z, S.layers[li], ws, src, src_a, cur, cur_a, B, L, pad,
                    posP + li * (size_t)R * HPD, temb, li + 1 < S.layers.size(), s, li > 0);
@@ -1377,7 +1389,7 @@ struct zv_engine {
       const StackW& S = Z.stacks[si];
       const float* te = tstack ? tstack + si * (size_t)N * D : nullptr;
       if (S.ds == 1) {
-        stack<SPLIT>(Z, S, ws, main, main_a, N, T, pad, te, s);
+        stack<SPLIT>(Z, S, (int)si, ws, main, main_a, N, T, pad, te, s);
       } else {
         const int dL = (T + S.ds - 1) / S.ds;
         float* d = ws.dsrc.get<float>((size_t)N * dL * D);
@@ -1392,7 +1404,7 @@ struct zv_engine {
                              N, T, dL, S.ds);
           ZV_LAUNCH_CHECK();
         }
-        stack<SPLIT>(Z, S, ws, d, d_a, N, dL, pds, te, s);
+        stack<SPLIT>(Z, S, (int)si, ws, d, d_a, N, dL, pds, te, s);
         if (D % 4 == 0 && 256 % (D / 4) == 0) {   // row blocks of whole rows (f32x4 per thread)
           const long rows_per_block = 4L * (256 / (D / 4));
           hipLaunchKernelGGL(zv_upsample_combine_kernel,
@@ -1420,8 +1432,12 @@ struct zv_engine {
     const bool split = cfg.precision == ZV_FP32 || cfg.precision == ZV_MIXED;   // split input projection
     const long N = (long)copies * B;
     Act xin = ws.xin.get(N * T, round_up(Fin, 64), split);
-    hipLaunchKernelGGL(zv_build_input_kernel, grid1d(N * T * Fin), dim3(256), 0, s, x, tc, sc,
-                       xin.h, xin.l, xin.ld, B, T, Fx, Ft, Fx, copies, zero_speech);
+    if (Fx % 4 == 0 && Ft % 4 == 0 && xin.ld % 4 == 0)
+      hipLaunchKernelGGL(zv_build_input4_kernel, grid1d(N * T * Fin / 4), dim3(256), 0, s, x, tc, sc,
+                         xin.h, xin.l, xin.ld, B, T, Fx, Ft, Fx, copies, zero_speech);
+    else
+      hipLaunchKernelGGL(zv_build_input_kernel, grid1d(N * T * Fin), dim3(256), 0, s, x, tc, sc,
+                         xin.h, xin.l, xin.ld, B, T, Fx, Ft, Fx, copies, zero_speech);
     ZV_LAUNCH_CHECK();
     return xin;
   }
@@ -1552,9 +1568,14 @@ struct zv_engine {
                   const std::vector<float>& ts, float g, const float* grows, bool cfg_rows,
                   hipStream_t s) {
     const int num_step = (int)ts.size() - 1;
-    for (int k = 0; k < num_step; ++k)
+    // steps after the first reuse the stacks' positional projections (same shapes and row
+    // blocks every step; a graph replays the first step's launches)
+    struct Reset { bool& f; ~Reset() { f = false; } } reset{posp_reuse};
+    for (int k = 0; k < num_step; ++k) {
+      posp_reuse = k > 0;
       velocity(ts[k], g, grows, cfg_rows, x, tc, sc, pad, B, T, nullptr, true, ts[k + 1] - ts[k],
                s);
+    }
   }
 
   // zv_euler_sample body: graph replay when possible, plain launches otherwise
