@@ -329,6 +329,27 @@ struct zv_engine {
            p.ldb >= round_up(p.K, GEMM_BK) && p.Brows >= p.N &&
            (long)cdiv(p.M, 256) * cdiv(p.N, 256) >= gemm256_min_tiles;
   }
+  // Residual linears (counted ROLE 1 / 2 / 4 / 5 epilogues): the tile by how many 128 x 128 tiles
+  // the launch has.  These linears are HBM-bound in the epilogue; a grid of fewer tiles than
+  // ~1.5 per CU leaves CUs idle or single-block, and smaller tiles with more blocks per CU
+  // overlap one block's residual traffic with the others' K loops.  Bitwise equal (every
+  // accumulator sees the same MFMA sequence).  Lab, K = 560 ROLE 4 (profiles/r05_resid_tiles_ab.txt):
+  // M = 6502 14.1 -> 12.4 us (128 x 64), 1625 11.1 -> 6.8 us (64 x 64); 13003 and up: 128 x 128
+  template <int SPLIT, int ROLE>
+  void launch_resid(const GemmParams& p, hipStream_t s, const char* tag) {
+    const long t = (long)cdiv(p.M, 128) * cdiv(p.N, 128), cus = zv_num_cus();
+    if constexpr (SPLIT == 1) {
+      if (t < cus / 2) {
+        launch_gemm<64, 64, 2, 2, SPLIT, EPI_STD, 4, 2, GEMM_BK, 0, 0, 0, ROLE>(p, 1, s, tag, true, gridx_resid);
+        return;
+      }
+      if (t < cus * 3 / 2) {
+        launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD, 2, 3, GEMM_BK, 0, 0, 0, ROLE>(p, 1, s, tag, true, gridx_resid);
+        return;
+      }
+    }
+    launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, ROLE>(p, 1, s, tag, true, gridx_resid);
+  }
   // ---------------------------------------------------------------- HIP graphs
   // The whole N-step Euler solve (~250 launches per step) is captured once per
   // (shape, schedule) on an engine-owned stream over engine-owned staging copies
@@ -905,7 +926,7 @@ struct zv_engine {
         // the copy-only form (no fp32 output) on the counted epilogue (A/B ZV_SA_COPY)
         if (sa_copy && !p.C && p.rowvec && !p.orig && !o.act.l && !o.act.q && p.Ch && p.bias &&
             Lw.N % 8 == 0 && p.ldch % 8 == 0) {
-          if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 5>(p, 1, s, "gemm_bf16_resid_copy", true, gridx_resid);
+          if (occ_resid == 2) launch_resid<SPLIT, 5>(p, s, "gemm_bf16_resid_copy");
           else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 5>(p, 1, s, "gemm_bf16_resid_copy", true, gridx_resid);
           return false;
         }
@@ -920,7 +941,7 @@ struct zv_engine {
         else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1>(p, 1, s, rtag, true, gridx_resid);
       } else if (p.orig) {           // one tag per ROLE: the roofline's bytes and PMC traffic per symbol
         const char* t2 = SPLIT == 3 ? "gemm_fp32_resid_byp" : "gemm_bf16_resid_byp";
-        if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 2>(p, 1, s, t2, true, gridx_resid);
+        if (occ_resid == 2) launch_resid<SPLIT, 2>(p, s, t2);
         else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 2>(p, 1, s, t2, true, gridx_resid);
       } else if (p.rowvec) {         // + the row-group vector (ROLE 4)
         rtag = SPLIT == 3 ? "gemm_fp32_resid_rv" : "gemm_bf16_resid_rv";
@@ -930,10 +951,10 @@ struct zv_engine {
             launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 4, 1>(p, 1, s, rtag, true, gridx_resid);
             return true;
           }
-        if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 4>(p, 1, s, rtag, true, gridx_resid);
+        if (occ_resid == 2) launch_resid<SPLIT, 4>(p, s, rtag);
         else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 4>(p, 1, s, rtag, true, gridx_resid);
       } else {
-        if (occ_resid == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 1>(p, 1, s, rtag, true, gridx_resid);
+        if (occ_resid == 2) launch_resid<SPLIT, 1>(p, s, rtag);
         else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 1>(p, 1, s, rtag, true, gridx_resid);
       }
       return false;
@@ -966,7 +987,11 @@ struct zv_engine {
         return false;
       }
     if (counted) {
-      if (occ_plain == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, tag, true, gridx_plain);
+      // (fewer than 1.5 128 x 128 tiles per CU: 128 x 64 tiles, 3 blocks per CU; bitwise equal;
+      // lab 3660 x 1536 x 512 13.7 -> 12.9 us, 1830 rows 10.5 -> 9.0, r05_resid_tiles_ab.txt)
+      if (occ_plain == 2 && SPLIT == 1 && (long)cdiv(p.M, 128) * cdiv(p.N, 128) < zv_num_cus() * 3 / 2)
+        launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD, 2, 3, GEMM_BK, 0, 0, 0, 3>(p, 1, s, tag, true, gridx_plain);
+      else if (occ_plain == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, tag, true, gridx_plain);
       else launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 1, GEMM_BK, 0, 0, 0, 3>(p, 1, s, tag, true, gridx_plain);
     } else if (occ_plain == 2) {
       launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2>(p, 1, s, tag, true, gridx_plain);
