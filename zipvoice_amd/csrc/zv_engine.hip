@@ -971,6 +971,11 @@ struct zv_engine {
         launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, SPLIT == 3 ? "gemm_fp32_n96" : "gemm_bf16_n96", true, gridx_plain);
         return false;
       }
+      if (cnt && n96_mode == 2 && SPLIT == 1 && (long)cdiv(p.M, 128) * cdiv(p.N, 128) < zv_num_cus() * 3 / 2) {
+        // (small launches: 128 x 64, 3 blocks per CU, as launch_resid)
+        launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD, 2, 3, GEMM_BK, 0, 0, 0, 3>(p, 1, s, "gemm_bf16_n96", true, gridx_plain);
+        return false;
+      }
       if (cnt && n96_mode == 2) {
         launch_gemm<128, 128, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, SPLIT == 3 ? "gemm_fp32_n96" : "gemm_bf16_n96", true, gridx_plain);
         return false;
@@ -1133,8 +1138,13 @@ struct zv_engine {
       // counted NA epilogue: 16-bit modes (in the split mode it differs from the general one
       // by up to 1.1e-4 in the decoder output, tools/counted_bisect.py; not bitwise: kept off)
       if (done) {}
-      else if ((res_counted & 4) && SPLIT == 1 && occ_fused == 2 && p.bias && W.na_in.N % 48 == 0 && p.ldch % 4 == 0)
-        launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
+      else if ((res_counted & 4) && SPLIT == 1 && occ_fused == 2 && p.bias && W.na_in.N % 48 == 0 && p.ldch % 4 == 0) {
+        // (fewer than 1.5 128 x 96 tiles per CU: 64-row tiles, 3 blocks per CU)
+        if ((long)cdiv(p.M, 128) * cdiv(p.N, 96) < zv_num_cus() * 3 / 2)
+          launch_gemm<64, 96, 2, 2, SPLIT, EPI_NA, 2, 3, GEMM_BK, 0, 0, 0, 3>(p, 1, s, "gemm_bf16_na", true, gridx_fused);
+        else
+          launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
+      }
       else if (occ_fused == 2) launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       else launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 1>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
       Act nao = ws.na_o.get(M, round_up(hid, 64), split, f8, hid);
@@ -1267,8 +1277,13 @@ struct zv_engine {
           done = true;
         }
       if (done) {}
-      else if ((res_counted & 8) && occ_fused == 2 && p.bias && W.conv_in[c].N % 32 == 0 && p.ldch % 8 == 0)
-        launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
+      else if ((res_counted & 8) && occ_fused == 2 && p.bias && W.conv_in[c].N % 32 == 0 && p.ldch % 8 == 0) {
+        // (fewer than 1.5 128 x 128 tiles per CU: 64 x 128, 3 blocks per CU, as launch_resid)
+        if (SPLIT == 1 && (long)cdiv(p.M, 128) * cdiv(p.N, 128) < zv_num_cus() * 3 / 2)
+          launch_gemm<64, 128, 2, 2, SPLIT, EPI_GLU, 2, 3, GEMM_BK, 0, 0, 0, 3>(p, 1, s, "gemm_bf16_glu", true, gridx_fused);
+        else
+          launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
+      }
       else if (occ_fused == 2) launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 2>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       else launch_gemm<128, 128, 2, 2, SPLIT, EPI_GLU, 2, 1>(p, 1, s, split ? "gemm_fp32_glu" : "gemm_bf16_glu", true, gridx_fused);
       Act dw = kcat ? dwo : ws.dw.get(M, D, split, f8, D);
