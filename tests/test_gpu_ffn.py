@@ -10,7 +10,7 @@ the fp32 oracle (reference zipformer.py:1433-1439, :610-618; scaling.py:330-355)
 other (the kernel itself matches the unfused pair to 2e-7: tools/lab/ffn_lab,
 profiles/r03_ffn_lab.txt).  The pipelined depthwise conv keeps the register-window kernel's FMA
 order per output: bitwise equal velocities.  ZV_FFN_MIN_ROWS=0 puts every launch on the fused
-kernel (by default launches under 10000 rows keep the unfused pair)."""
+kernel (by default launches under 15000 rows keep the unfused pair)."""
 import numpy as np
 import pytest
 

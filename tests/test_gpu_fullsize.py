@@ -97,7 +97,7 @@ def test_velocity_full_size_vs_oracle(name, precision):
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_velocity_full_size_fp16_fused_ff(monkeypatch, name):
     """The fp16 parity mode with the fused FeedForward on every launch (ZV_FFN_MIN_ROWS=0; by
-    default launches of a batch under 10000 rows keep the unfused pair, and these B <= 2 shapes
+    default launches of a batch under 15000 rows keep the unfused pair, and these B <= 2 shapes
     would never reach the kernel the bench runs) at every config's real length, held to
     north_star's 1e-3 mean bar with no escape."""
     variant, B, T, lens, Fx, t, g = CASES[name]
@@ -121,7 +121,7 @@ def test_c2_batch_rows_equal_single_utterance(monkeypatch):
     """The C2 bench shape (32 utterances = 64 CFG rows, T = 1219, bf16): each row of the
     batched velocity equals the single-utterance run (rows are independent: no
     cross-row arithmetic anywhere on the path), and row 0 matches the oracle.  The
-    FeedForward kernel is chosen by launch rows (fused from ZV_FFN_MIN_ROWS = 10000 rows
+    FeedForward kernel is chosen by launch rows (fused from ZV_FFN_MIN_ROWS = 15000 rows
     by default), so a batch-invariant engine pins the choice: ZV_FFN_MIN_ROWS=0."""
     B, T = 32, 1219
     x, tc, sc, pm = inputs(B, T, 100, [T] * B, seed=21)

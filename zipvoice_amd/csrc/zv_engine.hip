@@ -274,8 +274,10 @@ struct zv_engine {
   // (profiles/r03_ffn_configs_ab.txt).  The choice follows the launch's rows, so an
   // utterance's rounding can depend on its batch (as any shape-dependent kernel choice);
   // ZV_FFN_MIN_ROWS=0 pins the fused kernel for a batch-invariant engine
-  // (tests/test_gpu_fullsize.py batch rows test)
-  long ffn_min_rows = 10000;
+  // (tests/test_gpu_fullsize.py batch rows test).  10k -> 15k in round 5, after the small-launch
+  // tiles sped up the pair: C5's half-rate stacks (13.5k rows) 183.6 -> 176.2 ms per step; C2 /
+  // C3 / C4 have no stack in [10k, 15k) (profiles/r05_ffn_min_rows_ab.txt)
+  long ffn_min_rows = 15000;
   int fp8_fuse = 7;                // ZV_FP8_FUSE (fp8 mode): which bf16 producers write the fp8 copy
                                    // themselves (2 depthwise conv, 4 BiasNorm; bit 1 is unused since
                                    // the wave-specialised epilogue's removal); the others are followed
@@ -309,7 +311,7 @@ struct zv_engine {
     sa_tp = envi("ZV_SA_TP", 1);
     fp8_fuse = envi("ZV_FP8_FUSE", 7);
     ffn_fused = envi("ZV_FFN", 2);
-    ffn_min_rows = envi("ZV_FFN_MIN_ROWS", 10000);
+    ffn_min_rows = envi("ZV_FFN_MIN_ROWS", 15000);
     ffn_persist = envi("ZV_FFN_PERSIST", 1);
     res_counted = envi("ZV_RES_COUNTED", 31);
     if (res_counted == 1) res_counted = 31;            // 1: all (0 / 1 are the A/B tests' arms)
