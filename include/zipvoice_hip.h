@@ -120,6 +120,31 @@ int zv_profile_report(char* buf, int buflen);
  * zipvoice/models/modules/solver.py:213-240, runs eagerly on the caller's stream). */
 int64_t zv_host_block_count(void);
 
+/* Exact-path counters of the second-generation attention consumers of the bf16 / fp8 engines
+ * (csrc/zv_flash2.inc).  Those kernels take p = 2^s without subtracting a row maximum; a
+ * SelfAttention wave or NonlinAttention block whose range check fails redoes its queries with the
+ * maximum subtracted (the reference's softmax, zipformer.py:1257-1306).  host_counts[0]: runs with
+ * a query denominator under 2^-60, [1]: over 2^100 or a non-finite accumulator, [2]: every run
+ * (including those forced by ZV_ATTN2_EXACT=1, test infrastructure).  Synchronises the device;
+ * reset = 1 zeroes the counters.  No reference counterpart (the reference materialises softmax). */
+int zv_attn_fallbacks(zv_handle h, int reset, int64_t* host_counts);
+
+/* The second-generation attention consumers alone, on host arrays (test infrastructure: pins
+ * csrc/zv_flash2.inc against a float64 softmax in tests/test_gpu_attn2.py).  Inputs are rounded to
+ * the bf16 operand format as the engine's producers round them.  qkp (B, L, 2*32*H + 4*H) fp32 rows
+ * [q | k | p] in base-2 units (the engine folds log2(e) into the k / p weights); P (2L-1, 4*H) the
+ * positional projection (base 2); key_pad (B, L) 1 = padded, or NULL (masked_fill(-1000) of
+ * zipformer.py:1281-1289 in base 2).  kernel 0 = SelfAttention (zipformer.py:1359-1396): v (B, L,
+ * H*nv), nv <= 12, out (B, L, H*nv); kernel 1 = NonlinAttention (zipformer.py:1499-1544, head 0):
+ * v, y, out (B, L, nv), out = y * (W0 . v).  form 0 = the engine's choice for L (SelfAttention 1 / 2:
+ * register-fed with 2 / 3 query tiles per wave, 3 / 4 / 5: LDS-ring with 2 / 3 / 4; NonlinAttention
+ * 1 / 2: 4 / 8 query tiles per block).  force_exact = 1 sends every wave / block through the exact
+ * path; counts (or NULL) receives the three zv_attn_fallbacks counters of this launch.  bf16 library
+ * only; synchronous. */
+int zv_attn2_check(int kernel, int form, int B, int L, int H, int nv, const float* qkp, const float* P,
+                   const uint8_t* key_pad, const float* v, const float* y, int force_exact, float* out,
+                   int64_t* counts);
+
 /* GEMM microbenchmark (random bf16 operands): average ms per launch of tile
  * variant `variant` (+100: one tile per block instead of the persistent grid) for
  * C(M,N) = A(M,K) W(N,K)^T with out_mode 0 = fp32 C, 1 = bf16 C, 2 = residual

@@ -157,6 +157,9 @@ struct Workspace {
   // the stack's length and weights only; Engine::posp_reuse)
   static constexpr int POSP_STACKS = 8;
   DBuf posPs[POSP_STACKS];
+  // what each posPs slot holds (written with it): a later step reuses it only on a match
+  struct PosPKey { int L = -1, nl = 0; const void* w = nullptr; const void* buf = nullptr; };
+  PosPKey posk[POSP_STACKS];
   size_t bytes() const {
     size_t s = 0;
     for (const DBuf& b : posPs) s += b.bytes;
@@ -303,6 +306,11 @@ struct zv_engine {
   // (zv_flash2.inc): log2(e) folded into the attention-score projection's k / p rows, the
   // SelfAttention value projection padded to 16 rows per head (ones row 12), no statistics pass
   bool attn_b2 = false;
+  // ZV_ATTN2_EXACT (test infrastructure, default 0): every second-generation consumer wave / block
+  // takes its exact path (row maximum subtracted) instead of only those whose range check fails
+  int attn2_exact = 0;
+  // exact-path counters of the second-generation consumers (FlashParams::fallback; zv_attn_fallbacks)
+  unsigned* attn_fallback = nullptr;
 
   explicit zv_engine(const zv_config& c) : cfg(c) {
     auto envi = [](const char* k, int d) { const char* v = getenv(k); return v ? atoi(v) : d; };
@@ -321,6 +329,7 @@ struct zv_engine {
     gemm256 = envi("ZV_GEMM256", 2);
     mixed_sa = envi("ZV_MIXED_SA", 1) != 0;
     attn_b2 = envi("ZV_ATTN2", 1) != 0 && (cfg.precision == ZV_BF16 || cfg.precision == ZV_FP8);
+    attn2_exact = envi("ZV_ATTN2_EXACT", 0) != 0;
   }
   // the 256x256 kernel's preconditions (16-bit operands: the lo halves the fp32-accurate mode
   // keeps beside them are not read; padded K rows, the direct
@@ -407,6 +416,25 @@ struct zv_engine {
   void ffn_site(FfnParams q, Workspace& ws, hipStream_t s, const char* tag) {
     attach_ffn_scratch(q, ws);
     launch_ffn(q, s, tag);
+  }
+
+  // the device error word (zv_dev_err_word) read without synchronising: a fused FeedForward C item
+  // that outwaited its producer finished on unwritten tiles, so the results of the calls since the
+  // last check are invalid.  Let every launch drain, clear the persistent schedule's flag words
+  // (a late producer may have left its flag set for a later launch), report once
+  void check_dev_err() {
+    volatile unsigned* e = zv_dev_err_host();
+    if (*e == 0) return;
+    ZV_CHECK(ZV_BLOCKING(hipDeviceSynchronize()));
+    auto clear = [](Workspace& w) {
+      if (w.ffn_flag.p) ZV_CHECK(ZV_BLOCKING(hipMemset(w.ffn_flag.p, 0, w.ffn_flag.bytes)));
+    };
+    clear(ws_dec); clear(ws_txt);
+    for (Workspace& w : ws_split) clear(w);
+    ZV_CHECK(ZV_BLOCKING(hipDeviceSynchronize()));
+    *e = 0;
+    throw std::runtime_error("fused FeedForward: a C item waited more than 2 s for its producer's tiles; "
+                             "the outputs of the calls since the previous one are invalid (schedule flags reset)");
   }
 
   void drop_graphs() {
@@ -768,6 +796,8 @@ struct zv_engine {
       fr[k] = expf((float)(-log(10000.0)) * (float)k / (float)half);
     temb_freqs = dalloc<float>(half);
     ZV_CHECK(ZV_BLOCKING(hipMemcpy(temb_freqs, fr.data(), half * sizeof(float), hipMemcpyHostToDevice)));
+    attn_fallback = dalloc<unsigned>(4);
+    ZV_CHECK(ZV_BLOCKING(hipMemset(attn_fallback, 0, 4 * sizeof(unsigned))));
     // strict=True: nothing left over
     size_t expected = count_expected();
     if (expected != staged.size())
@@ -1075,6 +1105,7 @@ struct zv_engine {
     } else {
       fp.qh = qkp.h; fp.ql = qkp.l; fp.ldq = qkpN; fp.P = posP; fp.key_pad = pad;
       fp.B = B; fp.L = L; fp.H = H;
+      fp.force_exact = attn2_exact; fp.fallback = attn_fallback;
       if (!a2) {
         fp.stats = ws.stats.get<float2>((size_t)M);     // head 0 only (NonlinAttention)
         if constexpr (SPLIT == 1)
@@ -1377,7 +1408,13 @@ struct zv_engine {
     const size_t pn = (size_t)std::max(nl, 1) * R * HPD;
     const bool own = si >= 0 && si < Workspace::POSP_STACKS;
     float* posP = own ? ws.posPs[si].get<float>(pn) : ws.posP.get<float>(pn);
-    if (!(own && posp_reuse)) {
+    bool reuse = false;
+    if (own) {
+      Workspace::PosPKey& k = ws.posk[si];
+      reuse = posp_reuse && k.L == L && k.nl == nl && k.w == S.pos_w_all && k.buf == posP;
+      k = Workspace::PosPKey{L, nl, S.pos_w_all, posP};
+    }
+    if (!reuse) {
       hipLaunchKernelGGL(zv_posp_kernel, dim3((unsigned)cdiv((long)nl * R * HPD, 256L)), dim3(256), 0, s, S.pos_w_all, posP,
                          L, nl, HPD, Z.pos_dim);
       ZV_LAUNCH_CHECK();
@@ -1753,6 +1790,7 @@ struct zv_engine {
 static void check_ready(zv_handle h) {
   ZV_REQUIRE(h != nullptr, "null engine handle");
   ZV_REQUIRE(h->ready, "engine weights not finalized (call zv_finalize)");
+  h->check_dev_err();
 }
 
 // GEMM microbenchmark on random operands: C(M,N) fp32 = A(M,K) . W(N,K)^T
@@ -1859,6 +1897,18 @@ int zv_reserve(zv_handle h, int max_batch, int max_frames) {
     throw;
   }
   release();
+  ZV_API_END
+}
+
+int zv_attn_fallbacks(zv_handle h, int reset, int64_t* host_counts) {
+  ZV_API_BEGIN
+  check_ready(h);
+  ZV_REQUIRE(host_counts != nullptr, "null counts");
+  unsigned c[4] = {0, 0, 0, 0};
+  ZV_CHECK(ZV_BLOCKING(hipDeviceSynchronize()));
+  ZV_CHECK(ZV_BLOCKING(hipMemcpy(c, h->attn_fallback, sizeof c, hipMemcpyDeviceToHost)));
+  for (int i = 0; i < 3; ++i) host_counts[i] = c[i];
+  if (reset) ZV_CHECK(ZV_BLOCKING(hipMemset(h->attn_fallback, 0, sizeof c)));
   ZV_API_END
 }
 
@@ -2016,6 +2066,116 @@ int zv_attn_plan(int split, int sa_plo, int tpm, int L, int nv_na, int64_t* lds_
   *lds_na = (int64_t)(split == 1 ? na_lds_bytes_for<1>(L, nv_na, tpm) : na_lds_bytes_for<3>(L, nv_na, tpm));
   *lds_stats = (int64_t)pos_mask_bytes(L, 64, true);
   *fits = split == 1 ? fused_attn_fits<1>(L, nv_na, sa_plo, tpm) : fused_attn_fits<3>(L, nv_na, sa_plo, tpm);
+  ZV_API_END
+}
+
+// Second-generation attention consumers on the device, alone (test infrastructure; host pointers).
+// Inputs are rounded to the 16-bit operand format here, exactly as the engine's producers round
+// them: qkp (B, L, 2 H 32 + 4 H) fp32 = [q | k | p] per row in base-2 units (the engine folds
+// log2(e) into the k / p weights), P (2L - 1, 4 H) the positional projection (also base 2), key_pad
+// (B, L) or null.  kernel 0 SelfAttention: v (B, L, H * nv), nv <= 12, out (B, L, H * nv);
+// kernel 1 NonlinAttention (head 0): v (B, L, nv), y (B, L, nv), out (B, L, nv) = y * (W0 . v).
+// form 0: the engine's choice for L; SelfAttention 1 / 2: sa2 with 2 / 3 query tiles per wave,
+// 3 / 4 / 5: sa3 with 2 / 3 / 4; NonlinAttention 1 / 2: 4 / 8 query tiles per block.
+// force_exact: every wave / block on its exact path.  counts (or null): zv_attn_fallbacks's three.
+int zv_attn2_check(int kernel, int form, int B, int L, int H, int nv, const float* qkp, const float* P,
+                   const uint8_t* key_pad, const float* v, const float* y, int force_exact, float* out,
+                   int64_t* counts) {
+  ZV_API_BEGIN
+  ZV_REQUIRE(std::string(ZV_OPERAND_NAME) == "bf16", "zv_attn2_check: the bf16-operand library");
+  ZV_REQUIRE((kernel == 0 || kernel == 1) && B > 0 && L > 0 && H > 0 && qkp && P && v && out &&
+                 (kernel == 0 ? (nv > 0 && nv <= 12) : (nv > 0 && nv <= 384 && y)),
+             "zv_attn2_check: bad arguments");
+  const long ldq = 2L * H * ATT_QD + H * ATT_PD, M = (long)B * L, Lpad = round_up(L, 64);
+  const long vrows = kernel == 0 ? 16L * H : nv;   // V^T rows per utterance
+  std::vector<bf16> hq((size_t)M * ldq), hv((size_t)B * vrows * Lpad, (bf16)0.f);
+  for (size_t i = 0; i < hq.size(); ++i) hq[i] = (bf16)qkp[i];
+  for (int b = 0; b < B; ++b)
+    for (long r = 0; r < vrows; ++r) {
+      const int h = kernel == 0 ? (int)(r / 16) : 0, d = kernel == 0 ? (int)(r % 16) : (int)r;
+      for (int j = 0; j < L; ++j) {
+        float x = 0.f;
+        if (kernel == 1) x = v[((long)b * L + j) * nv + d];
+        else if (d < nv) x = v[((long)b * L + j) * H * nv + (long)h * nv + d];
+        else if (d == 12) x = 1.f;                       // the ones row (softmax denominator)
+        hv[((size_t)b * vrows + r) * Lpad + j] = (bf16)x;
+      }
+    }
+  std::vector<bf16> hy;
+  if (kernel == 1) {
+    hy.resize((size_t)M * nv);
+    for (size_t i = 0; i < hy.size(); ++i) hy[i] = (bf16)y[i];
+  }
+  const long ocols = kernel == 0 ? (long)H * nv : nv, ldo = round_up(ocols, 8);
+  bf16 *dq = nullptr, *dv = nullptr, *dy = nullptr, *dout = nullptr;
+  float* dP = nullptr;
+  uint8_t* dpad = nullptr;
+  unsigned* dcnt = nullptr;
+  auto release = [&]() {
+    for (void* ptr : {(void*)dq, (void*)dv, (void*)dy, (void*)dout, (void*)dP, (void*)dpad, (void*)dcnt})
+      if (ptr) (void)ZV_BLOCKING(hipFree(ptr));
+  };
+  try {
+    ZV_CHECK(ZV_BLOCKING(hipMalloc(&dq, hq.size() * 2)));
+    ZV_CHECK(ZV_BLOCKING(hipMalloc(&dv, hv.size() * 2)));
+    ZV_CHECK(ZV_BLOCKING(hipMalloc(&dout, (size_t)M * ldo * 2)));
+    ZV_CHECK(ZV_BLOCKING(hipMalloc(&dP, (size_t)(2 * L - 1) * H * ATT_PD * 4)));
+    ZV_CHECK(ZV_BLOCKING(hipMalloc(&dcnt, 16)));
+    ZV_CHECK(ZV_BLOCKING(hipMemcpy(dq, hq.data(), hq.size() * 2, hipMemcpyHostToDevice)));
+    ZV_CHECK(ZV_BLOCKING(hipMemcpy(dv, hv.data(), hv.size() * 2, hipMemcpyHostToDevice)));
+    ZV_CHECK(ZV_BLOCKING(hipMemcpy(dP, P, (size_t)(2 * L - 1) * H * ATT_PD * 4, hipMemcpyHostToDevice)));
+    ZV_CHECK(ZV_BLOCKING(hipMemset(dout, 0, (size_t)M * ldo * 2)));
+    ZV_CHECK(ZV_BLOCKING(hipMemset(dcnt, 0, 16)));
+    if (key_pad) {
+      ZV_CHECK(ZV_BLOCKING(hipMalloc(&dpad, (size_t)M)));
+      ZV_CHECK(ZV_BLOCKING(hipMemcpy(dpad, key_pad, (size_t)M, hipMemcpyHostToDevice)));
+    }
+    if (kernel == 1) {
+      ZV_CHECK(ZV_BLOCKING(hipMalloc(&dy, hy.size() * 2)));
+      ZV_CHECK(ZV_BLOCKING(hipMemcpy(dy, hy.data(), hy.size() * 2, hipMemcpyHostToDevice)));
+    }
+    FlashParams f{};
+    f.qh = dq; f.ldq = ldq; f.P = dP; f.key_pad = dpad; f.B = B; f.L = L; f.H = H;
+    f.vh = dv; f.ldv = Lpad; f.sv_b = vrows * Lpad; f.nv = nv;
+    f.oh = dout; f.ldo = ldo;
+    f.force_exact = force_exact; f.fallback = dcnt;
+    hipStream_t s = nullptr;
+    if (kernel == 0) {
+      f.vrows_per_head = 16; f.ocol_per_head = nv;
+      const int fm = form ? form : (sa3_qpw(L) == 4 ? 5 : sa3_qpw(L) == 3 ? 4 : sa3_qpw(L) == 2 ? 3 : sa2_qpw(L) == 3 ? 2 : 1);
+      switch (fm) {
+        case 1: launch_attn_sa2<2>(f, s); break;
+        case 2: launch_attn_sa2<3, 1>(f, s); break;
+        case 3: launch_attn_sa3<2>(f, s); break;
+        case 4: launch_attn_sa3<3>(f, s); break;
+        case 5: launch_attn_sa3<4>(f, s); break;
+        default: throw std::invalid_argument("zv_attn2_check: SelfAttention form 0..5");
+      }
+    } else {
+      f.vrows_per_head = 0; f.ocol_per_head = 0;
+      f.mulh = dy; f.ldmul = nv;
+      const int fm = form ? form : (na2_qtiles(L) == 4 ? 1 : 2);
+      ZV_REQUIRE(fm == 1 || fm == 2, "zv_attn2_check: NonlinAttention form 0..2");
+      if (nv <= 128) { if (fm == 1) launch_attn_na2<1, 4>(f, s); else launch_attn_na2<1>(f, s); }
+      else if (nv <= 256) { if (fm == 1) launch_attn_na2<2, 4>(f, s); else launch_attn_na2<2>(f, s); }
+      else if (fm == 1) launch_attn_na2<3, 4>(f, s);
+      else launch_attn_na2<3>(f, s);
+    }
+    ZV_CHECK(ZV_BLOCKING(hipDeviceSynchronize()));
+    std::vector<bf16> ho((size_t)M * ldo);
+    ZV_CHECK(ZV_BLOCKING(hipMemcpy(ho.data(), dout, ho.size() * 2, hipMemcpyDeviceToHost)));
+    for (long m = 0; m < M; ++m)
+      for (long c = 0; c < ocols; ++c) out[m * ocols + c] = (float)ho[m * ldo + c];
+    if (counts) {
+      unsigned c[4];
+      ZV_CHECK(ZV_BLOCKING(hipMemcpy(c, dcnt, 16, hipMemcpyDeviceToHost)));
+      for (int i = 0; i < 3; ++i) counts[i] = c[i];
+    }
+  } catch (...) {
+    release();
+    throw;
+  }
+  release();
   ZV_API_END
 }
 

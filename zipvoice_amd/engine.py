@@ -74,6 +74,8 @@ SIGNATURES = {
     "zv_gemm_selftest": (_I, [_I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]),
     "zv_profile_report": (_I, [ctypes.c_char_p, _I]),
     "zv_host_block_count": (ctypes.c_int64, []),
+    "zv_attn_fallbacks": (_I, [_P, _I, _P]),
+    "zv_attn2_check": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P, _P]),
     "zv_attn_plan": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "zv_mx8_quantize": (_I, [_P, _I, _I, _P, _P]),
     "zv_mx8_gemm_check": (_I, [_I, _I, _I, _P, _P, _P, _P, _P]),
@@ -271,6 +273,14 @@ class HipEngine:
 
     def device_bytes(self) -> int:
         return int(self.lib.zv_device_bytes(self.h))
+
+    def attn_fallbacks(self, reset: bool = False) -> tuple:
+        """(low, high, total) exact-path runs of the second-generation attention consumers since
+        the last reset (zv_attn_fallbacks; synchronises the device)."""
+        c = (ctypes.c_int64 * 3)()
+        with torch.cuda.device(self.device):
+            self._check(self.lib.zv_attn_fallbacks(self.h, int(reset), ctypes.cast(c, ctypes.c_void_p)))
+        return int(c[0]), int(c[1]), int(c[2])
 
     # ------------------------------------------------------------------ ops
     def fm_decoder(self, t: torch.Tensor, xt, text_c, speech_c, padding_mask=None,
