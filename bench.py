@@ -12,6 +12,14 @@ pretrained weights offline) and synthetic inputs of the configs' shapes:
 * C3 (``--config C3``, BASELINE configs[2]): ZipVoice-Distill, N_steps=8, guidance
   3.0 through the guidance embedding (no CFG doubling), a fixed global batch of 128
   utterances of the same shape sharded over the N GPUs (strong scaling).
+* C4 (``--config C4``, BASELINE configs[3]): ZipVoice-Dialog, N_steps=16, 16 dialogues per
+  GPU, each a 6 s prompt (563 frames, 80 tokens) + 30 s generated (2813 frames, 400 tokens,
+  speaker turns [S1] / [S2]), T = 3376, CFG 1.5 (32 decoder rows per GPU); weak scaling.
+* C5 (``--config C5``, BASELINE configs[4]): ZipVoice-Dialog-Stereo, N_steps=16, a fixed
+  global batch of 32 two-channel dialogues of C4's shape (200-dim features) sharded over the
+  N GPUs (4 per GPU on 8), CFG 1.5, fp8 MFMA weights by default (``--precision fp8``, the
+  BASELINE mode; bf16 selectable); each channel decoded by the vocoder
+  (``infer_zipvoice_dialog.py:478-490``), wav (B, n, 2).
 
 One "step" = what the reference's RTF times (``infer_zipvoice.py:359-386``) for the
 whole global batch, run data-parallel (``zipvoice_amd.dist.generate_batch_dp``):
@@ -21,7 +29,7 @@ vocoder on the generated features (post-processing + Vocos decode + clamp, ``:37
 and one RCCL all-gather over xGMI reassembles the output wav batch on every rank.
 Inputs are resident in HBM before the timed region.
 
-Launch: python bench.py [--gpus N --steps K --warmup W --config C2|C3]
+Launch: python bench.py [--gpus N --steps K --warmup W --config C2|C3|C4|C5 --precision P]
         (N > 1 under torch.distributed.run, one process per GPU).
 """
 import argparse
@@ -36,26 +44,40 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-# per-utterance shape of C2/C3
-T_PROMPT = 281
-S_PROMPT = 40
-S_TEXT = 134
-T_GEN = 938
+# per-utterance shapes: C2 / C3 3 s prompt + 10 s generated; C4 / C5 6 s + 30 s
+SHAPE_10S = dict(t_prompt=281, s_prompt=40, s_text=134, t_gen=938)
+SHAPE_30S = dict(t_prompt=563, s_prompt=80, s_text=400, t_gen=2813)
 T_SHIFT = 0.5
 SAMPLE_RATE = 24000
 HOP = 256
 CONFIGS = {
     "C2": dict(variant="zipvoice", num_step=16, guidance=1.0, per_gpu=32, global_batch=None,
-               scaling="weak", cfg_rows=2,
+               scaling="weak", cfg_rows=2, precision="bf16", **SHAPE_10S,
+               metric="generated mel-frames/s (whole job) + RTF, ZipVoice 123M N_steps=16 batch=32/GPU",
                desc="C2: ZipVoice 123M, N_steps=16, batch=32/GPU x (3 s prompt + 10 s generated; "
                     "T=1219 frames), CFG g=1.0 (64 decoder rows per GPU), t_shift=0.5"),
     "C3": dict(variant="zipvoice_distill", num_step=8, guidance=3.0, per_gpu=None,
-               global_batch=128, scaling="strong", cfg_rows=1,
+               global_batch=128, scaling="strong", cfg_rows=1, precision="bf16", **SHAPE_10S,
+               metric="generated mel-frames/s (whole job) + RTF, ZipVoice-Distill N_steps=8 batch=128",
                desc="C3: ZipVoice-Distill 123M, N_steps=8, global batch=128 x (3 s prompt + 10 s "
                     "generated; T=1219 frames) sharded over the GPUs, guidance 3.0 (embedding, "
                     "no CFG doubling), t_shift=0.5"),
+    "C4": dict(variant="zipvoice_dialog", num_step=16, guidance=1.5, per_gpu=16, global_batch=None,
+               scaling="weak", cfg_rows=2, precision="bf16", **SHAPE_30S,
+               metric="generated mel-frames/s (whole job) + RTF, ZipVoice-Dialog N_steps=16 batch=16x30s/GPU",
+               desc="C4: ZipVoice-Dialog, N_steps=16, batch=16/GPU x (6 s prompt + 30 s generated "
+                    "dialogue with [S1]/[S2] turns; T=3376 frames), CFG g=1.5 (32 decoder rows per "
+                    "GPU), t_shift=0.5"),
+    "C5": dict(variant="zipvoice_dialog_stereo", num_step=16, guidance=1.5, per_gpu=None,
+               global_batch=32, scaling="strong", cfg_rows=2, precision="fp8", **SHAPE_30S,
+               metric="generated mel-frames/s (whole job, per channel) + RTF, ZipVoice-Dialog-Stereo "
+                      "N_steps=16 batch=32 two-channel",
+               desc="C5: ZipVoice-Dialog-Stereo, N_steps=16, global batch=32 two-channel dialogues x "
+                    "(6 s prompt + 30 s generated; T=3376 frames, 200-dim features) sharded over "
+                    "the GPUs, CFG g=1.5, t_shift=0.5; both channels vocoded"),
 }
 BF16_DENSE_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: ~2.5 PF dense bf16
+FP8_DENSE_PEAK_TFLOPS = 5000.0      # ... ~5 PF dense fp8 (the MX-fp8 GEMMs of the fp8 mode)
 FP32_MFMA_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
 # PMC traffic per launch (tools/pmc_traffic.py) of the kernels the roofline reports, keyed by
@@ -80,26 +102,39 @@ def decoder_flops(T):
 VOCODER_FLOPS_PER_FRAME = 27e6
 
 
-def item_arrays(i):
-    """Utterance i of the synthetic global batch (the same on every rank)."""
+def feat_width(conf):
+    return 200 if conf["variant"] == "zipvoice_dialog_stereo" else 100
+
+
+def item_arrays(conf, i):
+    """Utterance i of the synthetic global batch (the same on every rank).  Dialog configs put
+    the speaker-turn tokens [S1] (360) / [S2] (361) at the start and the middle of both texts."""
     rng = np.random.default_rng([1000, i])
-    tokens = [int(v) for v in rng.integers(1, 360, S_TEXT)]
-    ptokens = [int(v) for v in rng.integers(1, 360, S_PROMPT)]
-    pf = (0.3 * rng.standard_normal((T_PROMPT, 100)) - 0.5).astype(np.float32)
-    x0 = np.random.default_rng([666, i]).standard_normal((T_PROMPT + T_GEN, 100),
+    dialog = conf["variant"].startswith("zipvoice_dialog")
+
+    def toks(n):
+        t = [int(v) for v in rng.integers(1, 360, n)]
+        if dialog:
+            t[0], t[n // 2] = 360, 361
+        return t
+
+    tokens, ptokens = toks(conf["s_text"]), toks(conf["s_prompt"])
+    F = feat_width(conf)
+    pf = (0.3 * rng.standard_normal((conf["t_prompt"], F)) - 0.5).astype(np.float32)
+    x0 = np.random.default_rng([666, i]).standard_normal((conf["t_prompt"] + conf["t_gen"], F),
                                                          dtype=np.float32)
     return tokens, ptokens, pf, x0
 
 
-def materialize(ids, device):
+def materialize(conf, ids, device):
     """Device-resident inputs of a shard (built before the timed region)."""
-    arrs = [item_arrays(i) for i in ids]
+    arrs = [item_arrays(conf, i) for i in ids]
     b = len(ids)
     to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
     return dict(tokens=[a[0] for a in arrs], prompt_tokens=[a[1] for a in arrs],
                 prompt_features=to(np.stack([a[2] for a in arrs])) if b else None,
-                prompt_features_lens=to(np.full(b, T_PROMPT, np.int64)),
-                features_lens=to(np.full(b, T_GEN, np.int64)),
+                prompt_features_lens=to(np.full(b, conf["t_prompt"], np.int64)),
+                features_lens=to(np.full(b, conf["t_gen"], np.int64)),
                 x0=to(np.stack([a[3] for a in arrs])) if b else None)
 
 
@@ -125,16 +160,17 @@ class Job:
         from zipvoice_amd.dist import shard_bounds, _world_rank
         self.conf, self.model, self.vocoder, self.device = conf, model, vocoder, device
         self.items = list(range(n_items))
-        self.costs = [T_PROMPT + T_GEN] * n_items      # frames per utterance
+        self.costs = [conf["t_prompt"] + conf["t_gen"]] * n_items      # frames per utterance
         world, rank = _world_rank()
         lo, hi = shard_bounds(self.costs, world)[rank]
-        self.inp = materialize(self.items[lo:hi], device)
+        self.inp = materialize(conf, self.items[lo:hi], device)
         self.n_local = hi - lo
+        self.channels = 2 if feat_width(conf) == 200 else 1
 
     def compute(self, shard):
         assert len(shard) == self.n_local
         if not shard:
-            return (torch.zeros((0, 1), device=self.device),
+            return (torch.zeros((0, 1) if self.channels == 1 else (0, 1, self.channels), device=self.device),
                     torch.zeros((0,), dtype=torch.int64, device=self.device))
         inp = self.inp
         gen, gen_lens, _, _ = self.model.sample(
@@ -143,9 +179,18 @@ class Job:
             prompt_features_lens=inp["prompt_features_lens"],
             features_lens=inp["features_lens"], t_shift=T_SHIFT, duration="real",
             num_step=self.conf["num_step"], guidance_scale=self.conf["guidance"], x0=inp["x0"])
-        wav = self.vocoder.decode_features(gen, gen_lens, feat_scale=0.1, feat_bias=0.0,
-                                           clamp=True)
-        return wav, gen_lens * HOP
+        if self.channels == 1:
+            wav = self.vocoder.decode_features(gen, gen_lens, feat_scale=0.1, feat_bias=0.0,
+                                               clamp=True)
+            return wav, gen_lens * HOP
+        # two-channel features: each channel decoded (infer_zipvoice_dialog.py:478-490), both in
+        # one vocoder batch, returned channel-last (b, n, 2)
+        b = gen.shape[0]
+        F = gen.shape[2] // 2
+        both = torch.cat([gen[..., :F], gen[..., F:]], 0)
+        wav = self.vocoder.decode_features(both, torch.cat([gen_lens, gen_lens]), feat_scale=0.1,
+                                           feat_bias=0.0, clamp=True)
+        return wav.view(2, b, -1).permute(1, 2, 0), gen_lens * HOP
 
     def step(self):
         from zipvoice_amd.dist import generate_batch_dp
@@ -184,7 +229,8 @@ def _kernel_roofline(name, r, total_ms):
         achieved, peak, unit = r["bytes"] / sec / 1e9, HBM_PEAK_GBS, "GB/s"
     else:
         achieved = r["flops"] / sec / 1e12
-        peak = BF16_DENSE_PEAK_TFLOPS if "bf16" in name else FP32_MFMA_PEAK_TFLOPS
+        peak = (FP8_DENSE_PEAK_TFLOPS if "fp8" in name else
+                BF16_DENSE_PEAK_TFLOPS if "bf16" in name else FP32_MFMA_PEAK_TFLOPS)
         unit = "TFLOP/s"
     traffic, tsrc = None, None
     tfile = next((f for f in TRAFFIC_FILES.get(name, [])
@@ -245,10 +291,11 @@ def roofline(job):
     return res
 
 
-def cpu_baseline(variant, guidance, num_step, budget_s=12.0):
+def cpu_baseline(conf, budget_s=12.0):
     """Oracle (numpy fp32 restatement, oracle/zipvoice_np.py) on the host cores: one
-    utterance of the same workload (T=1219; CFG batch of 2 where the model guides),
-    velocity evaluations repeated until ~budget_s, scaled to generated frames/s."""
+    utterance of the same workload (the config's T and feature width; CFG batch of 2 where the
+    model guides), velocity evaluations repeated until ~budget_s, scaled to generated frames/s."""
+    variant, guidance, num_step = conf["variant"], conf["guidance"], conf["num_step"]
     from threadpoolctl import threadpool_limits
 
     from oracle.zipvoice_np import ZipVoiceOracle
@@ -258,10 +305,10 @@ def cpu_baseline(variant, guidance, num_step, budget_s=12.0):
     cfg = default_config(variant)
     o = ZipVoiceOracle(cfg, synthetic_state_dict(cfg, 0))
     rng = np.random.default_rng(7)
-    T = T_PROMPT + T_GEN
-    x = rng.standard_normal((1, T, 100), dtype=np.float32)
+    T, T_GEN, F = conf["t_prompt"] + conf["t_gen"], conf["t_gen"], feat_width(conf)
+    x = rng.standard_normal((1, T, F), dtype=np.float32)
     tc = rng.standard_normal((1, T, 100), dtype=np.float32)
-    sc = rng.standard_normal((1, T, 100), dtype=np.float32)
+    sc = rng.standard_normal((1, T, F), dtype=np.float32)
     pm = np.zeros((1, T), bool)
     n = 0
     with threadpool_limits(limits=cores):
@@ -286,11 +333,14 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp16", "fp8"])
+    ap.add_argument("--precision", default=None, choices=["bf16", "fp32", "fp16", "fp8"],
+                    help="compute mode (default: the config's, bf16; C5 fp8 as BASELINE names it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fp32-mode", action="store_true")
     args = ap.parse_args()
     conf = CONFIGS[args.config]
+    if args.precision is None:
+        args.precision = conf["precision"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -306,18 +356,17 @@ def main():
     vocoder = build_vocoder(device)
     job = Job(conf, model, vocoder, n_items, device)
     ms = timed(job, args.steps, args.warmup, world) * 1e3
+    T_GEN = conf["t_gen"]
     frames = n_items * T_GEN
     value = frames / (ms * 1e-3)
     audio_s = n_items * T_GEN * HOP / SAMPLE_RATE
     rtf = (ms * 1e-3) / audio_s                      # whole job
-    T = T_PROMPT + T_GEN
+    T = conf["t_prompt"] + T_GEN
     path_flops = (n_items * conf["cfg_rows"] * conf["num_step"] * decoder_flops(T)
-                  + n_items * T_GEN * VOCODER_FLOPS_PER_FRAME)
+                  + job.channels * n_items * T_GEN * VOCODER_FLOPS_PER_FRAME)
     path_tfs = path_flops / (ms * 1e-3) / 1e12
     result = {
-        "metric": "generated mel-frames/s (whole job) + RTF, ZipVoice 123M N_steps=16 batch=32/GPU"
-                  if args.config == "C2" else
-                  "generated mel-frames/s (whole job) + RTF, ZipVoice-Distill N_steps=8 batch=128",
+        "metric": conf["metric"],
         "value": round(value, 1), "unit": "mel-frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True,
         "scaling": conf["scaling"], "vs_baseline": None, "dtype": args.precision,
@@ -336,7 +385,7 @@ def main():
     }
     if rank == 0:
         result["roofline"] = roofline(job)
-        if world == 1 and not args.no_fp32_mode and args.precision == "bf16":
+        if world == 1 and not args.no_fp32_mode and args.precision == "bf16" and args.config in ("C2", "C3"):
             del job, model
             torch.cuda.empty_cache()
             m32 = build(conf["variant"], "fp32", device)
@@ -372,8 +421,7 @@ def main():
             # tree it runs within 2-4 % of bf16 (the explicit stop); its C5 timing is
             # tools/config_bench.py's, its accuracy tests/test_gpu_fp8.py
         if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(conf["variant"], conf["guidance"],
-                                                  conf["num_step"])
+            result["cpu_baseline"] = cpu_baseline(conf)
         print(json.dumps(result), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -78,25 +78,30 @@ def test_all_gather_reassembles_batch_world2():
             assert torch.all(allx[i, costs[i]:] == 0)
 
 
-def _dp_worker(rank, world, port, q):
+def _dp_worker(rank, world, port, q, n_items=9, channels=1):
     """generate_batch_dp — the function bench.py's data-parallel step runs — with a CPU
     compute stub in place of sample() + vocoder: utterance i yields costs[i] samples of
-    value i."""
+    value i (channels == 2: the stereo form, channel c = (-1)^c i, as bench.py's C5 step
+    returns (b, n, 2))."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from zipvoice_amd.dist import generate_batch_dp
-        items = list(range(9))
+        items = list(range(n_items))
         costs = [5 + (3 * i) % 7 for i in items]
         seen = []
 
         def compute(shard):
             seen.extend(shard)
             n = max([costs[i] for i in shard], default=1)
-            wav = torch.zeros((len(shard), n))
+            wav = torch.zeros((len(shard), n) if channels == 1 else (len(shard), n, channels))
             for j, i in enumerate(shard):
-                wav[j, :costs[i]] = float(i)
+                if channels == 1:
+                    wav[j, :costs[i]] = float(i)
+                else:
+                    for c in range(channels):
+                        wav[j, :costs[i], c] = float(i) * (-1) ** c
             return wav, torch.tensor([costs[i] for i in shard], dtype=torch.int64)
 
         wav, lens, (lo, hi) = generate_batch_dp(items, compute, costs)
@@ -105,29 +110,36 @@ def _dp_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_generate_batch_dp_world2():
+@pytest.mark.parametrize("n_items,channels", [(9, 1), (32, 2)], ids=["mono", "stereo-C5"])
+def test_generate_batch_dp_world2(n_items, channels):
+    """mono, and the C5 shape (bench.py --config C5: 32 Dialog-Stereo utterances, (b, n, 2))."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q, n_items, channels)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in procs])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    costs = [5 + (3 * i) % 7 for i in range(9)]
+    costs = [5 + (3 * i) % 7 for i in range(n_items)]
     # each rank computed exactly its own contiguous shard; together every item once
-    assert sorted(res[0][3] + res[1][3]) == list(range(9))
+    assert sorted(res[0][3] + res[1][3]) == list(range(n_items))
     assert res[0][3] == list(range(res[0][4], res[0][5]))
     assert res[0][5] == res[1][4]
     for rank, wav, lens, _, _, _ in res:
         assert lens == costs
         wav = torch.tensor(wav)
-        assert wav.shape[0] == 9
-        for i in range(9):
-            assert torch.all(wav[i, :costs[i]] == float(i))
-            assert torch.all(wav[i, costs[i]:] == 0)
+        assert wav.shape[0] == n_items and wav.dim() == (2 if channels == 1 else 3)
+        for i in range(n_items):
+            if channels == 1:
+                assert torch.all(wav[i, :costs[i]] == float(i))
+                assert torch.all(wav[i, costs[i]:] == 0)
+            else:
+                for c in range(channels):
+                    assert torch.all(wav[i, :costs[i], c] == float(i) * (-1) ** c)
+                assert torch.all(wav[i, costs[i]:] == 0)
 
 
 def test_generate_batch_dp_single_process():

@@ -86,7 +86,10 @@ def generate_batch_dp(items: Sequence, compute: Callable[[Sequence], Tuple[torch
     whole ``sample()`` + vocoder path; nothing crosses ranks inside it), and the single
     exchange of the path, :func:`all_gather_padded` (RCCL over xGMI on GPUs, gloo on CPU),
     reassembles the (B, n_max) wav batch and its lengths in the original item order on
-    every rank.  Returns (wav, lens, (lo, hi)) with (lo, hi) this rank's shard."""
+    every rank.  Multi-channel output (ZipVoice-Dialog-Stereo: one wav per channel,
+    ``infer_zipvoice_dialog.py:483-490``) comes as wav (b, n, C) channel-last with lens in
+    samples per channel and is gathered as (B, n_max, C).  Returns (wav, lens, (lo, hi)) with
+    (lo, hi) this rank's shard."""
     world, rank = _world_rank(group)
     if costs is None:
         costs = [1.0] * len(items)
@@ -94,9 +97,12 @@ def generate_batch_dp(items: Sequence, compute: Callable[[Sequence], Tuple[torch
         raise ValueError("costs must have one entry per item")
     lo, hi = shard_bounds(costs, world)[rank]
     wav, lens = compute(items[lo:hi])
-    if wav.dim() != 2 or lens.dim() != 1 or wav.shape[0] != lens.shape[0] or wav.shape[0] != hi - lo:
-        raise ValueError("compute must return (wav (b, n), lens (b,)) for its b = hi - lo items")
+    if (wav.dim() not in (2, 3) or lens.dim() != 1 or wav.shape[0] != lens.shape[0]
+            or wav.shape[0] != hi - lo):
+        raise ValueError("compute must return (wav (b, n) or (b, n, C), lens (b,)) for its "
+                         "b = hi - lo items")
     if world == 1:
         return wav, lens, (lo, hi)
-    out, olens = all_gather_padded(wav.unsqueeze(-1), lens, group)
-    return out.squeeze(-1), olens, (lo, hi)
+    mono = wav.dim() == 2
+    out, olens = all_gather_padded(wav.unsqueeze(-1) if mono else wav.contiguous(), lens, group)
+    return (out.squeeze(-1) if mono else out), olens, (lo, hi)
