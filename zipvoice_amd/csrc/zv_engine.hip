@@ -309,6 +309,9 @@ struct zv_engine {
   // ZV_ATTN2_EXACT (test infrastructure, default 0): every second-generation consumer wave / block
   // takes its exact path (row maximum subtracted) instead of only those whose range check fails
   int attn2_exact = 0;
+  // ZV_GLU_DW (default 1): the convolution module's GLU linear and depthwise conv (+ SwooshR) as one
+  // launch (zv_gemm256.inc g256_epi_glu_dw) in the 16-bit modes; bitwise equal to the pair
+  int glu_dw = 1;
   // exact-path counters of the second-generation consumers (FlashParams::fallback; zv_attn_fallbacks)
   unsigned* attn_fallback = nullptr;
 
@@ -330,6 +333,7 @@ struct zv_engine {
     mixed_sa = envi("ZV_MIXED_SA", 1) != 0;
     attn_b2 = envi("ZV_ATTN2", 1) != 0 && (cfg.precision == ZV_BF16 || cfg.precision == ZV_FP8);
     attn2_exact = envi("ZV_ATTN2_EXACT", 0) != 0;
+    glu_dw = envi("ZV_GLU_DW", 1);
   }
   // the 256x256 kernel's preconditions (16-bit operands: the lo halves the fp32-accurate mode
   // keeps beside them are not read; padded K rows, the direct
@@ -1294,8 +1298,34 @@ struct zv_engine {
       linear<SPLIT>(W.sa_out[a], o, M, e, s);         // (+ the stream's fp8 copy)
     };
     auto conv = [&](int c) {                          // ConvolutionModule (:1638-1680)
-      Act g = ws.glu.get(M, D, split);
       const bool g8 = f8 && W.conv_in[c].q8;
+      if constexpr (SPLIT == 1) {
+        // in_proj + GLU + masked_fill + depthwise conv + SwooshR in one launch: the GLU output
+        // never reaches HBM (zv_gemm256.inc, g256_epi_glu_dw)
+        const int ks = W.ks;
+        if (glu_dw && !f8 && D == 512 && W.conv_in[c].N == 2 * D && (ks == 7 || ks == 15 || ks == 31) &&
+            (res_counted & 8)) {
+          Act dw = kcat ? dwo : ws.dw.get(M, D, split, f8, D);
+          GemmParams p = gp_linear(W.conv_in[c], cur_a, M);
+          p.Ch = dw.h; p.ldch = dw.ld; p.rowmask = pad;
+          p.dw_w = W.dw_w[c]; p.dw_b = W.dw_b[c]; p.dw_out = dw.h; p.ld_dw = dw.ld; p.dw_L = L;
+          if (p.bias && !p.Cl && !p.As && p.lda % 8 == 0 && p.ldb % 8 == 0 && p.lda >= round_up(p.K, GEMM_BK) &&
+              p.ldb >= round_up(p.K, GEMM_BK) && p.Brows >= p.N && dw.ld % 8 == 0) {
+            if (ks == 31) launch_gemm256<EPI_GLU, 3, 0, 0, 1, 1, 31>(p, s, "gemm_bf16_glu_dw", false);
+            else if (ks == 15) launch_gemm256<EPI_GLU, 3, 0, 0, 1, 1, 15>(p, s, "gemm_bf16_glu_dw", false);
+            else launch_gemm256<EPI_GLU, 3, 0, 0, 1, 1, 7>(p, s, "gemm_bf16_glu_dw", false);
+            if (kcat) {                               // cur += [dw | o] . [conv_out | sa_out]^T + temb
+              Out e = res;
+              e.rowvec = temb; e.rowvec_ld = D; e.rows_per_group = L;
+              linear<SPLIT>(W.conv_sa_out[c], dw, M, e, s);
+            } else {
+              linear<SPLIT>(W.conv_out[c], dw, M, res, s);
+            }
+            return;
+          }
+        }
+      }
+      Act g = ws.glu.get(M, D, split);
       GemmParams p = g8 ? gp_linear8(W.conv_in[c], cur_a, M) : gp_linear(W.conv_in[c], cur_a, M);
       p.Ch = g.h; p.Cl = g.l; p.ldch = g.ld; p.rowmask = pad;
       bool done = false;
