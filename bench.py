@@ -84,13 +84,16 @@ HBM_PEAK_GBS = 8000.0
 # the engine's profiler tag (one symbol per tag since round 3: the residual linears by ROLE, the
 # fused FeedForward with / without the BiasNorm epilogue); newest measurement first
 # (round 4: measured on the timed three-stream schedule, the same launch set the roofline pass times)
-TRAFFIC_FILES = {"gemm_bf16_resid": ["r05_gemm_resid_r1_traffic.json", "r04_gemm_resid_r1_traffic.json"],
-                 "gemm_bf16_resid_rv": ["r05_gemm_resid_r4_traffic.json", "r04_gemm_resid_r4_traffic.json"],
-                 "gemm_bf16_resid_byp": ["r05_gemm_resid_r2_traffic.json", "r04_gemm_resid_r2_traffic.json"],
-                 "ffn_bf16": ["r05_ffn_traffic.json", "r04_ffn_traffic.json"],
-                 "ffn_norm_bf16": ["r05_ffn_norm_traffic.json", "r04_ffn_norm_traffic.json"],
-                 "ffn_bf16+ffn_norm_bf16": ["r05_ffn_all_traffic.json", "r04_ffn_all_traffic.json"],
-                 "gemm_bf16": ["r05_gemm_traffic.json", "r04_gemm_traffic.json"]}
+# (round 6: the residual ROLEs' regexes cover every tile form the tag launches -- 128 x 128, 128 x 64
+# and 64 x 64 -- so the PMC mean and the algorithmic mean describe the same launch set; the text
+# encoder pass is included, which is where ROLE 2 runs)
+TRAFFIC_FILES = {"gemm_bf16_resid": ["r06_gemm_resid_r1_traffic.json"],
+                 "gemm_bf16_resid_rv": ["r06_gemm_resid_r4_traffic.json"],
+                 "gemm_bf16_resid_byp": ["r06_gemm_resid_r2_traffic.json"],
+                 "ffn_bf16": ["r06_ffn_traffic.json", "r05_ffn_traffic.json"],
+                 "ffn_norm_bf16": ["r06_ffn_norm_traffic.json", "r05_ffn_norm_traffic.json"],
+                 "ffn_bf16+ffn_norm_bf16": ["r06_ffn_all_traffic.json", "r05_ffn_all_traffic.json"],
+                 "gemm_bf16_glu_dw": ["r06_gemm_glu_dw_traffic.json"]}
 # the residual-stream linears by epilogue ROLE (zv_gemm.inc): the HBM-bound family of the path
 RESID_TAGS = ("gemm_bf16_resid", "gemm_bf16_resid_rv", "gemm_bf16_resid_byp")
 # analytic FLOPs of one decoder sequence-forward (FlopCounterMode fit on the
@@ -286,7 +289,9 @@ def roofline(job):
     res = _kernel_roofline(name, r, total_ms)
     if len(ff) > 1:
         res["per_tag"] = {t: _kernel_roofline(t, rep[t], total_ms) for t in ff}
-    res["secondary"] = {t: _kernel_roofline(t, rep[t], total_ms) for t in RESID_TAGS if t in rep}
+    # (+ the fused convolution front, GLU linear + depthwise conv: MFMA + VALU, priced on the MFMA peak)
+    res["secondary"] = {t: _kernel_roofline(t, rep[t], total_ms) for t in RESID_TAGS + ("gemm_bf16_glu_dw",)
+                        if t in rep}
     res["per_kernel_ms_per_step"] = {k: round(v["ms"], 3) for k, v in rep.items()}
     return res
 

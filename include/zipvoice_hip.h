@@ -131,7 +131,7 @@ int zv_attn_fallbacks(zv_handle h, int reset, int64_t* host_counts);
 
 /* The second-generation attention consumers alone, on host arrays (test infrastructure: pins
  * csrc/zv_flash2.inc against a float64 softmax in tests/test_gpu_attn2.py).  Inputs are rounded to
- * the bf16 operand format as the engine's producers round them.  qkp (B, L, 2*32*H + 4*H) fp32 rows
+ * the operand format as the engine's producers round them.  qkp (B, L, 2*32*H + 4*H) fp32 rows
  * [q | k | p] in base-2 units (the engine folds log2(e) into the k / p weights); P (2L-1, 4*H) the
  * positional projection (base 2); key_pad (B, L) 1 = padded, or NULL (masked_fill(-1000) of
  * zipformer.py:1281-1289 in base 2).  kernel 0 = SelfAttention (zipformer.py:1359-1396): v (B, L,
@@ -139,8 +139,9 @@ int zv_attn_fallbacks(zv_handle h, int reset, int64_t* host_counts);
  * v, y, out (B, L, nv), out = y * (W0 . v).  form 0 = the engine's choice for L (SelfAttention 1 / 2:
  * register-fed with 2 / 3 query tiles per wave, 3 / 4 / 5: LDS-ring with 2 / 3 / 4; NonlinAttention
  * 1 / 2: 4 / 8 query tiles per block).  force_exact = 1 sends every wave / block through the exact
- * path; counts (or NULL) receives the three zv_attn_fallbacks counters of this launch.  bf16 library
- * only; synchronous. */
+ * path; counts (or NULL) receives the three zv_attn_fallbacks counters of this launch.  Operands
+ * are the library's (bf16; fp16 in libzipvoice_hip_f16.so, whose kernels take p = 2^(s - o) with a
+ * per-query offset o); synchronous. */
 int zv_attn2_check(int kernel, int form, int B, int L, int H, int nv, const float* qkp, const float* P,
                    const uint8_t* key_pad, const float* v, const float* y, int force_exact, float* out,
                    int64_t* counts);

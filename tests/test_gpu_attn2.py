@@ -38,20 +38,27 @@ MASKED = -1000.0 * LOG2E
 H, QD, PD = 4, 32, 4
 
 
-def bf16(a):
-    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(torch.bfloat16).float().numpy()
+def rounded(a, operand):
+    dt = torch.bfloat16 if operand == "bf16" else torch.float16
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dt).float().numpy()
 
 
-def make_inputs(B, L, kernel, nv, seed, straddle=False, ragged=True):
+def make_inputs(B, L, kernel, nv, seed, straddle=False, ragged=True, operand="bf16"):
     rng = np.random.default_rng(seed)
     q = 0.5 * rng.standard_normal((B, L, H, QD))
     k = 0.5 * rng.standard_normal((B, L, H, QD))
     p = 0.5 * rng.standard_normal((B, L, H, PD))
     if straddle:
-        # per-query shift r_i * 8 of every score (k dim 31 constant 8, q dim 31 = r_i): chunks of
+        # per-query shift r_i * 8 of the scores (k dim 31 constant 8, q dim 31 = r_i): chunks of
         # 128 queries at 0 / +40 / -40 / 0 ...: denominators 2^320 and 2^-320 beside normal ones
-        # (a NonlinAttention block holds at most 128 queries, a SelfAttention wave at most 64)
+        # (a NonlinAttention block holds at most 128 queries, a SelfAttention wave at most 64).
+        # fp16 operands: the kernels' per-query offset (the first key step's maximum) absorbs a
+        # shift of every key, so there only the keys past the first 64 are shifted: the +40 chunks'
+        # later scores rise 320 above the offset (overflow -> the exact path), the -40 chunks' fall
+        # 320 below it (their weights vanish, correctly, on the fast path)
         k[..., 31] = 8.0
+        if operand != "bf16":
+            k[:, :64, :, 31] = 0.0
         r = np.array([0.0, 40.0, -40.0, 0.0])[(np.arange(L) // 128) % 4]
         q[..., 31] = r[None, :, None]
     qkp = np.concatenate([q.reshape(B, L, H * QD), k.reshape(B, L, H * QD), p.reshape(B, L, H * PD)], -1)
@@ -65,7 +72,7 @@ def make_inputs(B, L, kernel, nv, seed, straddle=False, ragged=True):
     else:
         v = rng.standard_normal((B, L, nv))
         y = rng.standard_normal((B, L, nv))
-    return [bf16(a) if a is not None else None for a in (qkp, P, v, y)] + [pad]
+    return [rounded(a, operand) if a is not None else None for a in (qkp, P, v, y)] + [pad]
 
 
 def reference(qkp, P, v, y, pad, kernel, nv):
@@ -99,9 +106,9 @@ def reference(qkp, P, v, y, pad, kernel, nv):
     return out, mag
 
 
-def run_check(kernel, form, qkp, P, v, y, pad, nv, force_exact):
+def run_check(kernel, form, qkp, P, v, y, pad, nv, force_exact, operand="bf16"):
     from zipvoice_amd import engine
-    lib = engine.load_library()
+    lib = engine.load_library(operand="f16" if operand == "f16" else "bf16")
     B, L, _ = qkp.shape
     out = np.zeros((B, L, H * nv if kernel == 0 else nv), np.float32)
     cnt = (ctypes.c_int64 * 3)()
@@ -140,25 +147,31 @@ def units(kernel, form, B, L):
     return B * -(-L // NA_BLOCK_Q[form])
 
 
+@pytest.mark.parametrize("operand", ["bf16", "f16"])
 @pytest.mark.parametrize("regime", ["normal", "forced", "straddle"])
 @pytest.mark.parametrize("case", SA_CASES + NA_CASES, ids=lambda c: f"{'SA' if c[0] == 0 else 'NA'}-f{c[1]}-L{c[2]}")
-def test_attn2_kernel_vs_float64(case, regime):
+def test_attn2_kernel_vs_float64(case, regime, operand):
+    """operand f16: the same kernels in libzipvoice_hip_f16.so (the fp16 parity mode's decoder), with
+    the per-query offsets (zv_flash2.inc FA2_OFS)."""
     kernel, form, L = case
     nv = 12 if kernel == 0 else 384
     B = 2
-    qkp, P, v, y, pad = make_inputs(B, L, kernel, nv, seed=L * 10 + form, straddle=regime == "straddle")
-    out, cnt = run_check(kernel, form, qkp, P, v, y, pad, nv, force_exact=regime == "forced")
+    qkp, P, v, y, pad = make_inputs(B, L, kernel, nv, seed=L * 10 + form, straddle=regime == "straddle",
+                                    operand=operand)
+    out, cnt = run_check(kernel, form, qkp, P, v, y, pad, nv, force_exact=regime == "forced", operand=operand)
     ref, mag = reference(qkp, P, v, y, pad, kernel, nv)
     n = units(kernel, form, B, L)
-    print(f"{case} {regime}: exact-path runs (low, high, all) = {cnt} of {n}")
-    check_bound(out, ref, mag, f"{case} {regime}")
+    print(f"{case} {regime} [{operand}]: exact-path runs (low, high, all) = {cnt} of {n}")
+    check_bound(out, ref, mag, f"{case} {regime} [{operand}]")
     if regime == "normal":
         assert cnt == (0, 0, 0), cnt
     elif regime == "forced":
         assert cnt[2] == n and cnt[0] == cnt[1] == 0, (cnt, n)
-    else:
+    elif operand == "bf16":
         # both edges fire, and the waves / blocks of the unshifted chunks stay on the fast path
         assert cnt[0] > 0 and cnt[1] > 0 and cnt[2] < n, (cnt, n)
+    else:
+        assert cnt[1] > 0 and cnt[2] < n, (cnt, n)
 
 
 # ---------------------------------------------------------------------------------------------

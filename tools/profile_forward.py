@@ -20,6 +20,8 @@ ap.add_argument("--iters", type=int, default=2)
 ap.add_argument("--B", type=int, default=32)
 ap.add_argument("--T", type=int, default=1219)
 ap.add_argument("--report", action="store_true", help="per-shape event-profiler table")
+ap.add_argument("--text", action="store_true",
+                help="also one text-encoder pass of the batch (its residual linears include the bypass ROLE 2)")
 a = ap.parse_args()
 cfg = default_config("zipvoice")
 m = build_model(cfg, precision=a.precision)
@@ -33,6 +35,9 @@ sc = torch.from_numpy(rng.standard_normal((a.B, a.T, 100), dtype=np.float32)).to
 pm = torch.zeros(a.B, a.T, dtype=torch.bool, device=dev)
 for _ in range(a.iters):
     v = m.engine.velocity(0.3, 1.0, x, tc, sc, pm)
+    if a.text:                      # the C2 shape's text: 40 prompt + 134 text tokens + 1 pad
+        tok = torch.from_numpy(rng.integers(1, 360, (a.B, 175))).to(dev)
+        m.engine.text_encode(tok, torch.zeros(a.B, 175, dtype=torch.bool, device=dev))
 torch.cuda.synchronize()
 print("ok", float(v.abs().mean()))
 if a.report:

@@ -87,6 +87,9 @@ struct ZipformerW {
   std::vector<StackW> stacks;
   bool has_time = false, has_guid = false;
   Linear te0, te2, guid;    // fp32 small linears
+  // weights built for the second-generation attention consumers (zv_flash2.inc: log2(e) on the
+  // attention-score projection's k / p rows, 16-row value heads); its 16-bit layers launch them
+  bool b2 = false;
 };
 
 // bumped whenever a workspace buffer moves: captured HIP graphs bake in
@@ -302,10 +305,11 @@ struct zv_engine {
   // the families the emulation names for the random T = 203 input's 1.08e-3 -> 8.9e-4
   // (tools/precision_study.py --velocity, profiles/r04_precision_study_r04_velocity_T203.txt)
   bool mixed_sa = true;
-  // ZV_ATTN2 (bf16 / fp8 engines, default 1): second-generation attention consumers
-  // (zv_flash2.inc): log2(e) folded into the attention-score projection's k / p rows, the
-  // SelfAttention value projection padded to 16 rows per head (ones row 12), no statistics pass
-  bool attn_b2 = false;
+  // ZV_ATTN2 (default 1): second-generation attention consumers (zv_flash2.inc): log2(e) folded
+  // into the attention-score projection's k / p rows, the SelfAttention value projection padded to
+  // 16 rows per head (ones row 12), no statistics pass.  bf16 / fp8 engines: decoder and text
+  // encoder; the fp16 parity mode (ZV_MIXED): the decoder (its text encoder runs the split products)
+  bool attn_b2 = false, attn_b2_dec = false;
   // ZV_ATTN2_EXACT (test infrastructure, default 0): every second-generation consumer wave / block
   // takes its exact path (row maximum subtracted) instead of only those whose range check fails
   int attn2_exact = 0;
@@ -332,6 +336,7 @@ struct zv_engine {
     gemm256 = envi("ZV_GEMM256", 2);
     mixed_sa = envi("ZV_MIXED_SA", 1) != 0;
     attn_b2 = envi("ZV_ATTN2", 1) != 0 && (cfg.precision == ZV_BF16 || cfg.precision == ZV_FP8);
+    attn_b2_dec = attn_b2 || (envi("ZV_ATTN2", 1) != 0 && cfg.precision == ZV_MIXED);
     attn2_exact = envi("ZV_ATTN2_EXACT", 0) != 0;
     glu_dw = envi("ZV_GLU_DW", 1);
   }
@@ -659,8 +664,8 @@ struct zv_engine {
                        const std::vector<int>& ds, const std::vector<int>& layers,
                        const std::vector<int>& ks, std::vector<int> in_dims,
                        std::vector<int> out_dims, bool two_stream, int temb_dim, bool guid,
-                       bool fp8_layers = false) {
-    Z.dim = dim; Z.ff = ff; Z.heads = heads;
+                       bool fp8_layers = false, bool b2 = false) {
+    Z.dim = dim; Z.ff = ff; Z.heads = heads; Z.b2 = b2;
     Z.qd = cfg.query_head_dim; Z.pd = cfg.pos_head_dim; Z.vd = cfg.value_head_dim;
     Z.pos_dim = cfg.pos_dim; Z.temb_dim = temb_dim;
     ZV_REQUIRE(Z.qd == ATT_QD && Z.pd == ATT_PD, "engine supports query_head_dim=32, pos_head_dim=4");
@@ -696,7 +701,7 @@ struct zv_engine {
       for (int li = 0; li < layers[s]; ++li) {
         std::string lp = ep + "layers." + std::to_string(li) + ".";
         LayerW W;
-        W.attn_in = make_linear(attn_b2 ? stage_rows_scaled(lp + "self_attn_weights.in_proj", qkp, dim,
+        W.attn_in = make_linear(b2 ? stage_rows_scaled(lp + "self_attn_weights.in_proj", qkp, dim,
                                                             heads * Z.qd, qkp, 1.4426950408889634f)
                                         : lp + "self_attn_weights.in_proj",
                                 qkp, dim, true, false);
@@ -707,7 +712,7 @@ struct zv_engine {
         }
         for (int a = 0; a < 2; ++a) {
           std::string ap = lp + "self_attn" + std::to_string(a + 1) + ".";
-          if (attn_b2) {
+          if (b2) {
             ZV_REQUIRE(Z.vd <= 12, "value_head_dim <= 12 for the padded value heads");
             W.sa_in[a] = make_linear(stage_value_heads16(ap + "in_proj", heads, Z.vd, dim), heads * 16, dim,
                                      true, false);
@@ -786,11 +791,11 @@ struct zv_engine {
     std::vector<int> out_dims = stereo() ? std::vector<int>{2 * F, F} : std::vector<int>{F};
     build_zipformer(dec, "fm_decoder.", cfg.fm_decoder_dim, cfg.fm_decoder_feedforward_dim,
                     cfg.fm_decoder_num_heads, ds, nl, ks, in_dims, out_dims, stereo(),
-                    cfg.time_embed_dim, distill(), /*fp8_layers=*/true);
+                    cfg.time_embed_dim, distill(), /*fp8_layers=*/true, attn_b2_dec);
     build_zipformer(txt, "text_encoder.", cfg.text_encoder_dim, cfg.text_encoder_feedforward_dim,
                     cfg.text_encoder_num_heads, {1}, {cfg.text_encoder_num_layers},
                     {cfg.text_encoder_cnn_module_kernel}, {cfg.text_embed_dim}, {F}, false, -1,
-                    false);
+                    false, attn_b2);
     embed_table = upload_f32("embed.weight", (size_t)cfg.vocab_size * cfg.text_embed_dim);
     if (dialog()) spk_table = upload_f32("spk_embed.weight", (size_t)2 * F);
     // timestep-embedding frequencies, float32 as zipformer.py:56-60
@@ -1095,9 +1100,9 @@ struct zv_engine {
     // per-row softmax statistics and recompute scores inside each consumer
     const int sa_plo = (SPLIT == 1 && sa_tp) ? (io_split && mixed_plo ? 1 : 0) : -1;
     // second-generation consumers (zv_flash2.inc: base-2 scores from the log2(e)-scaled k / p
-    // weights, no running maximum, no statistics pass) wherever this engine's weights were
-    // built for them (attn_b2: bf16 / fp8 engines)
-    const bool a2 = SPLIT == 1 && attn_b2 && !io_split;
+    // weights, no running maximum, no statistics pass) wherever this stack's weights were built for
+    // them (Z.b2: the bf16 / fp8 engines, and the fp16 parity mode's decoder)
+    const bool a2 = SPLIT == 1 && Z.b2;
     const bool materialize = materialize_attn || (a2 ? !fused_attn2_fits(L, W.na_in.N / 3)
                                                      : !fused_attn_fits<SPLIT>(L, W.na_in.N / 3, sa_plo, tp_na ? 1 : 0));
     Act Wt;
@@ -2100,7 +2105,8 @@ int zv_attn_plan(int split, int sa_plo, int tpm, int L, int nv_na, int64_t* lds_
 }
 
 // Second-generation attention consumers on the device, alone (test infrastructure; host pointers).
-// Inputs are rounded to the 16-bit operand format here, exactly as the engine's producers round
+// Inputs are rounded to the library's 16-bit operand format here (bf16, or fp16 in
+// libzipvoice_hip_f16.so, whose kernels add the per-query offsets), as the engine's producers round
 // them: qkp (B, L, 2 H 32 + 4 H) fp32 = [q | k | p] per row in base-2 units (the engine folds
 // log2(e) into the k / p weights), P (2L - 1, 4 H) the positional projection (also base 2), key_pad
 // (B, L) or null.  kernel 0 SelfAttention: v (B, L, H * nv), nv <= 12, out (B, L, H * nv);
@@ -2112,7 +2118,6 @@ int zv_attn2_check(int kernel, int form, int B, int L, int H, int nv, const floa
                    const uint8_t* key_pad, const float* v, const float* y, int force_exact, float* out,
                    int64_t* counts) {
   ZV_API_BEGIN
-  ZV_REQUIRE(std::string(ZV_OPERAND_NAME) == "bf16", "zv_attn2_check: the bf16-operand library");
   ZV_REQUIRE((kernel == 0 || kernel == 1) && B > 0 && L > 0 && H > 0 && qkp && P && v && out &&
                  (kernel == 0 ? (nv > 0 && nv <= 12) : (nv > 0 && nv <= 384 && y)),
              "zv_attn2_check: bad arguments");
