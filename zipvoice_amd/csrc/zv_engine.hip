@@ -1012,8 +1012,10 @@ struct zv_engine {
         launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, SPLIT == 3 ? "gemm_fp32_n96" : "gemm_bf16_n96", true, gridx_plain);
         return false;
       }
-      if (cnt && n96_mode == 2 && SPLIT == 1 && (long)cdiv(p.M, 128) * cdiv(p.N, 128) < zv_num_cus() * 3 / 2) {
-        // (small launches: 128 x 64, 3 blocks per CU, as launch_resid)
+      if (cnt && n96_mode == 2 && SPLIT == 1) {
+        // 128 x 64 tiles at 3 blocks per CU (320 columns computed), at every size: 15.2 -> 13.9 ms per
+        // C2 step against 128 x 128 for the large launches (round 6, profiles/r06_n96_ab.txt; 64 x 64
+        // with a 4-deep ring 15.3); bitwise equal
         launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD, 2, 3, GEMM_BK, 0, 0, 0, 3>(p, 1, s, "gemm_bf16_n96", true, gridx_plain);
         return false;
       }
