@@ -339,6 +339,7 @@ struct zv_engine {
     attn_b2_dec = attn_b2 || (envi("ZV_ATTN2", 1) != 0 && cfg.precision == ZV_MIXED);
     attn2_exact = envi("ZV_ATTN2_EXACT", 0) != 0;
     glu_dw = envi("ZV_GLU_DW", 1);
+    resid_tile = envi("ZV_RESID_TILE", 0);
   }
   // the 256x256 kernel's preconditions (16-bit operands: the lo halves the fp32-accurate mode
   // keeps beside them are not read; padded K rows, the direct
@@ -355,10 +356,19 @@ struct zv_engine {
   // overlap one block's residual traffic with the others' K loops.  Bitwise equal (every
   // accumulator sees the same MFMA sequence).  Lab, K = 560 ROLE 4 (profiles/r05_resid_tiles_ab.txt):
   // M = 6502 14.1 -> 12.4 us (128 x 64), 1625 11.1 -> 6.8 us (64 x 64); 13003 and up: 128 x 128
+  int resid_tile = 0;   // (lab: ZV_RESID_TILE 1 = 128 x 64 at 3 blocks per CU, 2 = 64 x 64 ring 4, at every size)
   template <int SPLIT, int ROLE>
   void launch_resid(const GemmParams& p, hipStream_t s, const char* tag) {
     const long t = (long)cdiv(p.M, 128) * cdiv(p.N, 128), cus = zv_num_cus();
     if constexpr (SPLIT == 1) {
+      if (resid_tile == 1) {
+        launch_gemm<128, 64, 2, 2, SPLIT, EPI_STD, 2, 3, GEMM_BK, 0, 0, 0, ROLE>(p, 1, s, tag, true, gridx_resid);
+        return;
+      }
+      if (resid_tile == 2) {
+        launch_gemm<64, 64, 2, 2, SPLIT, EPI_STD, 4, 2, GEMM_BK, 0, 0, 0, ROLE>(p, 1, s, tag, true, gridx_resid);
+        return;
+      }
       if (t < cus / 2) {
         launch_gemm<64, 64, 2, 2, SPLIT, EPI_STD, 4, 2, GEMM_BK, 0, 0, 0, ROLE>(p, 1, s, tag, true, gridx_resid);
         return;
