@@ -339,7 +339,6 @@ struct zv_engine {
     attn_b2_dec = attn_b2 || (envi("ZV_ATTN2", 1) != 0 && cfg.precision == ZV_MIXED);
     attn2_exact = envi("ZV_ATTN2_EXACT", 0) != 0;
     glu_dw = envi("ZV_GLU_DW", 1);
-    na_tile = envi("ZV_NA_TILE", 0);
   }
   // the 256x256 kernel's preconditions (16-bit operands: the lo halves the fp32-accurate mode
   // keeps beside them are not read; padded K rows, the direct
@@ -357,7 +356,6 @@ struct zv_engine {
   // accumulator sees the same MFMA sequence).  Lab, K = 560 ROLE 4 (profiles/r05_resid_tiles_ab.txt):
   // M = 6502 14.1 -> 12.4 us (128 x 64), 1625 11.1 -> 6.8 us (64 x 64); 13003 and up: 128 x 128
   // (128 x 64 or 64 x 64 at every size lost in the C2 step, round 6: profiles/r06_resid_tile_ab.txt)
-  int na_tile = 0;      // (lab: ZV_NA_TILE 1 = the NA in-projection on 64 x 96 tiles at every size)
   template <int SPLIT, int ROLE>
   void launch_resid(const GemmParams& p, hipStream_t s, const char* tag) {
     const long t = (long)cdiv(p.M, 128) * cdiv(p.N, 128), cus = zv_num_cus();
@@ -1187,8 +1185,9 @@ struct zv_engine {
       // by up to 1.1e-4 in the decoder output, tools/counted_bisect.py; not bitwise: kept off)
       if (done) {}
       else if ((res_counted & 4) && SPLIT == 1 && occ_fused == 2 && p.bias && W.na_in.N % 48 == 0 && p.ldch % 4 == 0) {
-        // (fewer than 1.5 128 x 96 tiles per CU: 64-row tiles, 3 blocks per CU)
-        if (na_tile == 1 || (long)cdiv(p.M, 128) * cdiv(p.N, 96) < zv_num_cus() * 3 / 2)
+        // (64-row tiles at 3 blocks per CU at every size: 32.5 -> 31.4 ms per C2 step against 128-row
+        // tiles for the large launches, round 6, profiles/r06_ffn_rows_na_tile_ab.txt; bitwise equal)
+        if (SPLIT == 1)
           launch_gemm<64, 96, 2, 2, SPLIT, EPI_NA, 2, 3, GEMM_BK, 0, 0, 0, 3>(p, 1, s, "gemm_bf16_na", true, gridx_fused);
         else
           launch_gemm<128, 96, 2, 2, SPLIT, EPI_NA, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, split ? "gemm_fp32_na" : "gemm_bf16_na", true, gridx_fused);
