@@ -245,14 +245,14 @@ def _kernel_roofline(name, r, total_ms):
         traffic = t.get("traffic_bytes_per_launch")
         tsrc = (f"profiles/{tfile}: rocprofv3 PMC FETCH_SIZE(x2, gfx950) + WRITE_SIZE "
                 f"per launch of {t['kernel_regex']} over one guided forward")
-    alg = r["bytes"] / r["launches"]
+    alg = r["bytes"] / r["launches"] if r["launches"] else 0.0
     out = {
         "kernel": name, "bound": "hbm" if hbm else "mfma", "achieved": round(achieved, 2), "peak": peak,
         "unit": unit, "frac": round(achieved / peak, 4), "traffic": traffic,
         "traffic_unit": "bytes per launch", "traffic_source": tsrc,
         "algorithmic_bytes_per_launch": round(alg),
-        "traffic_over_algorithmic": round(traffic / alg, 3) if traffic else None,
-        "hbm_frac": round(alg / (r["ms"] * 1e-3 / r["launches"]) / 1e9 / HBM_PEAK_GBS, 4),
+        "traffic_over_algorithmic": round(traffic / alg, 3) if traffic and alg else None,
+        "hbm_frac": round(alg / (r["ms"] * 1e-3 / r["launches"]) / 1e9 / HBM_PEAK_GBS, 4) if r["ms"] else None,
         "launches_per_step": r["launches"], "avg_launch_us": round(r["ms"] * 1e3 / r["launches"], 2),
         "flops_per_launch": r["flops"] / r["launches"],
         "tflops_achieved": round(r["flops"] / sec / 1e12, 2),

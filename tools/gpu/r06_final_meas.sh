@@ -3,10 +3,12 @@
 # separate passes over one guided forward + one text-encoder pass on the bench's 3-stream schedule;
 # each tag's regex covers every tile instantiation the tag launches), the bench line (reads that
 # traffic), a rocprofv3 kernel trace + stats of a short bench run.   tools/gpu/r06_final_meas.sh OUT
+# (SKIP_PMC=1: keep the traffic files already in profiles/)
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r06_final}; mkdir -p $O
 step() { echo "== $1 $(date +%T)"; }
+if [ -z "$SKIP_PMC" ]; then
 step pmc
 RX='zv_gemm_kernel|zv_ffn_kernel|zv_gemm256_kernel'
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -f csv --kernel-include-regex "$RX" -d $O/pmc_fetch -o run -- python3 tools/profile_forward.py --iters 1 --text > $O/pmc_fetch.log 2>&1 || { tail -5 $O/pmc_fetch.log; exit 1; }
@@ -27,6 +29,7 @@ done
 cut -c1-240 $O/pmc_traffic.log
 rm -f $F $W
 cp $O/r06_*_traffic.json profiles/
+fi
 step bench
 timeout -k 10 500 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/bench.json'));r=d['roofline'];print(d['ms_per_step'],d['value'],r['kernel'],r['frac'],r['avg_launch_us'],r.get('traffic_over_algorithmic'));print({k:v['ms_per_step'] for k,v in d.items() if isinstance(v,dict) and 'ms_per_step' in v})"
