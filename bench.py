@@ -246,12 +246,21 @@ def _kernel_roofline(name, r, total_ms):
         tsrc = (f"profiles/{tfile}: rocprofv3 PMC FETCH_SIZE(x2, gfx950) + WRITE_SIZE "
                 f"per launch of {t['kernel_regex']} over one guided forward")
     alg = r["bytes"] / r["launches"] if r["launches"] else 0.0
+    ratio = round(traffic / alg, 3) if traffic and alg else None
+    if traffic and t.get("traffic_over_algorithmic"):
+        # the PMC pass's launch mix differs from the timed step's (text-encoder launches, row
+        # blocks): take the ratio on the PMC pass's own launch set and price this launch set with it
+        ratio = t["traffic_over_algorithmic"]
+        tsrc += (f"; ratio to the algorithmic bytes of that same launch set "
+                 f"({t['algorithmic_launches']} launches), applied to this step's launches "
+                 f"(measured mean {traffic / 1e6:.1f} MB per PMC launch)")
+        traffic = ratio * alg
     out = {
         "kernel": name, "bound": "hbm" if hbm else "mfma", "achieved": round(achieved, 2), "peak": peak,
         "unit": unit, "frac": round(achieved / peak, 4), "traffic": traffic,
         "traffic_unit": "bytes per launch", "traffic_source": tsrc,
         "algorithmic_bytes_per_launch": round(alg),
-        "traffic_over_algorithmic": round(traffic / alg, 3) if traffic and alg else None,
+        "traffic_over_algorithmic": ratio,
         "hbm_frac": round(alg / (r["ms"] * 1e-3 / r["launches"]) / 1e9 / HBM_PEAK_GBS, 4) if r["ms"] else None,
         "launches_per_step": r["launches"], "avg_launch_us": round(r["ms"] * 1e3 / r["launches"], 2),
         "flops_per_launch": r["flops"] / r["launches"],

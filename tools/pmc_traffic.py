@@ -6,7 +6,12 @@ on gfx950 FETCH_SIZE reports half the bytes of wide (16 B/lane, incl. LDS-DMA)
 streaming reads, so it is doubled here.  Writes the per-launch figure as JSON
 (consumed by bench.py's roofline "traffic").
 
-usage: pmc_traffic.py FETCH_CSV WRITE_CSV KERNEL_REGEX OUT_JSON"""
+With ALG_JSON (tools/profile_forward.py --alg-json over the same command) and the engine profiler
+TAG(s) the regex's symbols launch under ("a+b" for a union), the file also carries the algorithmic
+bytes per launch of that same launch set and their ratio, so bench.py need not compare the PMC mean
+with a different launch mix.
+
+usage: pmc_traffic.py FETCH_CSV WRITE_CSV KERNEL_REGEX OUT_JSON [ALG_JSON TAG[+TAG]]"""
 import csv
 import json
 import re
@@ -29,5 +34,15 @@ res = {"kernel_regex": pattern, "launches": [nf, nw],
        "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->B, mean per dispatch"}
 if f is not None and w is not None:
     res["traffic_bytes_per_launch"] = res["fetch_bytes_per_launch"] + res["write_bytes_per_launch"]
+if len(sys.argv) > 6 and "traffic_bytes_per_launch" in res:
+    alg = json.load(open(sys.argv[5]))
+    tags = sys.argv[6].split("+")
+    n = sum(alg[t]["launches"] for t in tags if t in alg)
+    b = sum(alg[t]["bytes"] for t in tags if t in alg)
+    res["algorithmic_tags"] = tags
+    res["algorithmic_launches"] = n
+    if n:
+        res["algorithmic_bytes_per_launch"] = b / n
+        res["traffic_over_algorithmic"] = round(res["traffic_bytes_per_launch"] * n / b, 3) if b else None
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res))

@@ -20,6 +20,9 @@ ap.add_argument("--iters", type=int, default=2)
 ap.add_argument("--B", type=int, default=32)
 ap.add_argument("--T", type=int, default=1219)
 ap.add_argument("--report", action="store_true", help="per-shape event-profiler table")
+ap.add_argument("--alg-json", default=None,
+                help="event-profile the --iters loop itself and write {tag: launches, bytes, flops}: the "
+                     "algorithmic bytes of the same launch set a PMC pass of this command counts")
 ap.add_argument("--text", action="store_true",
                 help="also one text-encoder pass of the batch (its residual linears include the bypass ROLE 2)")
 a = ap.parse_args()
@@ -33,6 +36,9 @@ x = torch.from_numpy(rng.standard_normal((a.B, a.T, 100), dtype=np.float32)).to(
 tc = torch.from_numpy(rng.standard_normal((a.B, a.T, 100), dtype=np.float32)).to(dev)
 sc = torch.from_numpy(rng.standard_normal((a.B, a.T, 100), dtype=np.float32)).to(dev)
 pm = torch.zeros(a.B, a.T, dtype=torch.bool, device=dev)
+if a.alg_json:
+    from zipvoice_amd import engine
+    engine.profile(True)
 for _ in range(a.iters):
     v = m.engine.velocity(0.3, 1.0, x, tc, sc, pm)
     if a.text:                      # the C2 shape's text: 40 prompt + 134 text tokens + 1 pad
@@ -40,6 +46,12 @@ for _ in range(a.iters):
         m.engine.text_encode(tok, torch.zeros(a.B, 175, dtype=torch.bool, device=dev))
 torch.cuda.synchronize()
 print("ok", float(v.abs().mean()))
+if a.alg_json:
+    import json
+    rep = engine.profile_report()
+    engine.profile(False)
+    json.dump({k: {f: r[f] for f in ("launches", "bytes", "flops")} for k, r in rep.items()},
+              open(a.alg_json, "w"), indent=1)
 if a.report:
     from zipvoice_amd import engine
     engine.profile(True, detail=True)
