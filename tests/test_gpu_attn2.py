@@ -52,13 +52,15 @@ def make_inputs(B, L, kernel, nv, seed, straddle=False, ragged=True, operand="bf
         # per-query shift r_i * 8 of the scores (k dim 31 constant 8, q dim 31 = r_i): chunks of
         # 128 queries at 0 / +40 / -40 / 0 ...: denominators 2^320 and 2^-320 beside normal ones
         # (a NonlinAttention block holds at most 128 queries, a SelfAttention wave at most 64).
-        # fp16 operands: the kernels' per-query offset (the first key step's maximum) absorbs a
-        # shift of every key, so there only the keys past the first 64 are shifted: the +40 chunks'
-        # later scores rise 320 above the offset (overflow -> the exact path), the -40 chunks' fall
-        # 320 below it (their weights vanish, correctly, on the fast path)
+        # fp16 operands: the kernels' per-query offset (the maximum over the first key step and
+        # the step holding the query's own tile) absorbs a shift of every key, so there only keys
+        # 64..127 are shifted -- in neither of those steps for the queries of the +40 / -40 chunks:
+        # the +40 chunks' scores there rise 320 above the offset (overflow -> the exact path), the
+        # -40 chunks' fall 320 below it (their weights vanish, correctly, on the fast path)
         k[..., 31] = 8.0
         if operand != "bf16":
-            k[:, :64, :, 31] = 0.0
+            k[..., 31] = 0.0
+            k[:, 64:128, :, 31] = 8.0
         r = np.array([0.0, 40.0, -40.0, 0.0])[(np.arange(L) // 128) % 4]
         q[..., 31] = r[None, :, None]
     qkp = np.concatenate([q.reshape(B, L, H * QD), k.reshape(B, L, H * QD), p.reshape(B, L, H * PD)], -1)
