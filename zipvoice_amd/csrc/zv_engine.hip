@@ -28,6 +28,10 @@
 #include "zv_elem.inc"
 #include "zv_flash.inc"
 #include "zv_flash2.inc"
+// K-ring depth of the fp16 parity mode's weight-split value projection (A/B builds)
+#ifndef ZV_WSPLIT_T_STAGES
+#define ZV_WSPLIT_T_STAGES 2
+#endif
 #include "../../include/zipvoice_hip.h"
 
 static thread_local std::string g_last_error;
@@ -1258,7 +1262,8 @@ struct zv_engine {
       // N = 48 (64 padded): 64-row tiles give 2x the blocks of a 128-row grid (one tile column)
       if (sa_split) {                    // fp16 parity mode: a . (w_hi + w_lo)
         ZV_REQUIRE(W.sa_in[a].lo && (res_counted & 16), "weight-split value projection");
-        launch_gemm<64, 64, 2, 2, 2, EPI_TRANS, 2, 2, GEMM_BK, 0, 0, 0, 3>(p, 1, s, "gemm_wsplit_t", true, -1);
+        launch_gemm<64, 64, 2, 2, 2, EPI_TRANS, ZV_WSPLIT_T_STAGES, ZV_WSPLIT_T_STAGES < 4 ? 2 : 1, GEMM_BK, 0, 0, 0, 3>(
+            p, 1, s, "gemm_wsplit_t", true, -1);
       } else if (skinny_tiles && (res_counted & 16))
         // (a 4-deep K ring: one 64-row tile per block has 8 K steps and little else in flight;
         // 2 -> 4 stages: 24.0 -> 18.9 ms per C2 step, profiles/r05_vt_stages_ab.txt)
