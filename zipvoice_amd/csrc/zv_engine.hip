@@ -28,9 +28,10 @@
 #include "zv_elem.inc"
 #include "zv_flash.inc"
 #include "zv_flash2.inc"
-// K-ring depth of the fp16 parity mode's weight-split value projection (A/B builds)
+// K-ring depth of the fp16 parity mode's weight-split value projection (A/B builds; 3: 25.3 ->
+// 21.6 ms per C2 step against 2, 4 stages at one block per CU 22.3, profiles/r06_wsplit_ab.txt)
 #ifndef ZV_WSPLIT_T_STAGES
-#define ZV_WSPLIT_T_STAGES 2
+#define ZV_WSPLIT_T_STAGES 3
 #endif
 #include "../../include/zipvoice_hip.h"
 
