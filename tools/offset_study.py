@@ -83,10 +83,10 @@ for W in records:                       # (H, B, L, L)
                     ov = overflow(lw, ks, kset)
                     nunit = (L + unit - 1) // unit
                     units = sum(ov[u * unit:(u + 1) * unit].any() for u in range(nunit))
-                    t = tot.setdefault((kind, name), [0, 0, 0, 0])
+                    t = tot.setdefault((kind, L, name), [0, 0, 0, 0])
                     t[0] += int(ov.sum()); t[1] += L; t[2] += int(units); t[3] += nunit
 print(f"# T={T}, one guided velocity (t=0.3, CFG rows 2), synthetic weights (seed 0); "
       f"{len(records)} attention-weight sets")
-print(f"{'consumer':8s} {'offset from':18s} {'queries over':>14s} {'units over':>14s}")
-for (kind, name), (nq, qt, nu, ut) in tot.items():
-    print(f"{kind:8s} {name:18s} {nq:7d}/{qt:<7d} {nu:6d}/{ut:<6d}")
+print(f"{'consumer':8s} {'L':>5s} {'offset from':18s} {'queries over':>14s} {'units over':>14s}")
+for (kind, L, name), (nq, qt, nu, ut) in sorted(tot.items()):
+    print(f"{kind:8s} {L:5d} {name:18s} {nq:7d}/{qt:<7d} {nu:6d}/{ut:<6d}")
