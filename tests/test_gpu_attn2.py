@@ -43,7 +43,7 @@ def rounded(a, operand):
     return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dt).float().numpy()
 
 
-def make_inputs(B, L, kernel, nv, seed, straddle=False, ragged=True, operand="bf16"):
+def make_inputs(B, L, kernel, nv, seed, straddle=False, ragged=True, operand="bf16", diagonal=False):
     rng = np.random.default_rng(seed)
     q = 0.5 * rng.standard_normal((B, L, H, QD))
     k = 0.5 * rng.standard_normal((B, L, H, QD))
@@ -63,6 +63,14 @@ def make_inputs(B, L, kernel, nv, seed, straddle=False, ragged=True, operand="bf
             k[:, 64:128, :, 31] = 8.0
         r = np.array([0.0, 40.0, -40.0, 0.0])[(np.arange(L) // 128) % 4]
         q[..., 31] = r[None, :, None]
+    if diagonal:
+        # the +40 chunks' queries score +320 on their OWN chunk's keys only (k dim 31 = 8 there):
+        # the fp16 offsets take the step holding the query tile, so no unit overflows there (with
+        # the first step alone every +40 unit would); other queries' weights on those keys vanish.
+        # bf16 has no offsets: the same chunks' denominators reach 2^320 (high edge)
+        chunk = (np.arange(L) // 128) % 4
+        k[..., 31] = np.where(chunk == 1, 8.0, 0.0)[None, :, None]
+        q[..., 31] = np.array([0.0, 40.0, -40.0, 0.0])[chunk][None, :, None]
     qkp = np.concatenate([q.reshape(B, L, H * QD), k.reshape(B, L, H * QD), p.reshape(B, L, H * PD)], -1)
     P = 0.5 * rng.standard_normal((2 * L - 1, H * PD))
     pad = np.zeros((B, L), np.uint8)
@@ -150,7 +158,7 @@ def units(kernel, form, B, L):
 
 
 @pytest.mark.parametrize("operand", ["bf16", "f16"])
-@pytest.mark.parametrize("regime", ["normal", "forced", "straddle"])
+@pytest.mark.parametrize("regime", ["normal", "forced", "straddle", "diagonal"])
 @pytest.mark.parametrize("case", SA_CASES + NA_CASES, ids=lambda c: f"{'SA' if c[0] == 0 else 'NA'}-f{c[1]}-L{c[2]}")
 def test_attn2_kernel_vs_float64(case, regime, operand):
     """operand f16: the same kernels in libzipvoice_hip_f16.so (the fp16 parity mode's decoder), with
@@ -159,7 +167,11 @@ def test_attn2_kernel_vs_float64(case, regime, operand):
     nv = 12 if kernel == 0 else 384
     B = 2
     qkp, P, v, y, pad = make_inputs(B, L, kernel, nv, seed=L * 10 + form, straddle=regime == "straddle",
-                                    operand=operand)
+                                    operand=operand, diagonal=regime == "diagonal",
+                                    # (diagonal: both utterances unpadded -- a padded utterance's
+                                    # tail queries have a masked diagonal step, so their offsets
+                                    # come from step 0 and another +40 chunk's keys overflow them)
+                                    ragged=regime != "diagonal")
     out, cnt = run_check(kernel, form, qkp, P, v, y, pad, nv, force_exact=regime == "forced", operand=operand)
     ref, mag = reference(qkp, P, v, y, pad, kernel, nv)
     n = units(kernel, form, B, L)
@@ -169,6 +181,15 @@ def test_attn2_kernel_vs_float64(case, regime, operand):
         assert cnt == (0, 0, 0), cnt
     elif regime == "forced":
         assert cnt[2] == n and cnt[0] == cnt[1] == 0, (cnt, n)
+    elif regime == "diagonal":
+        if operand == "bf16":
+            assert cnt[1] > 0 and cnt[2] < n, (cnt, n)
+        elif kernel == 0 and form in (2, 4):
+            # 48-query waves: a wave straddling a chunk edge takes its offset from the step of its
+            # first tile, outside the shifted chunk (exact path, counted)
+            assert cnt[2] < n, (cnt, n)
+        else:
+            assert cnt == (0, 0, 0), cnt
     elif operand == "bf16":
         # both edges fire, and the waves / blocks of the unshifted chunks stay on the fast path
         assert cnt[0] > 0 and cnt[1] > 0 and cnt[2] < n, (cnt, n)
