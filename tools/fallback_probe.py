@@ -2,7 +2,8 @@
 velocity at the C2 / C4 shapes, per precision mode: how often the range check fires on the
 synthetic weights (bf16: raw 2^s; fp16: per-query offsets from the first key step).
 
-    python tools/fallback_probe.py [bf16,fp16] [T ...]"""
+    python tools/fallback_probe.py [bf16,fp16] [T ...]     (ZV_PROBE_RAGGED=1: utterance lengths
+                                                           0.6-1.0 T, the rest padded)"""
 import os
 import sys
 
@@ -27,9 +28,14 @@ for mode in modes:
         rng = np.random.default_rng(T)
         x, tc, sc = (torch.from_numpy(rng.standard_normal((B, T, 100), dtype=np.float32)).to("cuda:0")
                      for _ in range(3))
+        pm = None
+        if os.environ.get("ZV_PROBE_RAGGED") == "1":
+            lens = (T * rng.uniform(0.6, 1.0, B)).astype(int)
+            lens[0] = T
+            pm = torch.from_numpy(np.arange(T)[None, :] >= lens[:, None]).to("cuda:0")
         for t in (0.1, 0.5, 0.9):
             m.engine.attn_fallbacks(reset=True)
-            m.engine.velocity(t, 1.0, x, tc, sc, None)
+            m.engine.velocity(t, 1.0, x, tc, sc, pm)
             print(f"{mode} T={T} B={B} t={t}: exact-path runs (low, high, all) = "
                   f"{m.engine.attn_fallbacks(reset=True)}", flush=True)
     del m
